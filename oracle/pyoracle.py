@@ -1,0 +1,157 @@
+"""ctypes binding for the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker / CPU baseline; the product path
+(magical-1_amd) never touches it.  See oracle/oracle.h for what the oracle
+restates and how it is pinned.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libmg_oracle.so")
+
+TASKS = {"MoveToRegion": 0, "MoveToCorner": 1, "ClusterColour": 2, "ClusterShape": 3, "MatchRegions": 4}
+PREPROCS = {None: 0, "LoRes4E": 1, "LoResStack": 2, "LoRes3EA": 3, "LoRes4A": 4, "LoResCHW4E": 5, "LoResCHW4A": 5}
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        d, i, u32, vp = ctypes.c_double, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p
+        L.o_crsin.restype = d; L.o_crsin.argtypes = [d]
+        L.o_crcos.restype = d; L.o_crcos.argtypes = [d]
+        L.o_crtan.restype = d; L.o_crtan.argtypes = [d]
+        L.oenv_create.restype = vp; L.oenv_create.argtypes = [i, i, i, i, u32]
+        L.oenv_destroy.argtypes = [vp]
+        L.oenv_seed.argtypes = [vp, u32]
+        L.oenv_obs_bytes.restype = i; L.oenv_obs_bytes.argtypes = [vp]
+        L.oenv_reset.restype = i; L.oenv_reset.argtypes = [vp, vp]
+        L.oenv_step.restype = i
+        L.oenv_step.argtypes = [vp, i, vp, ctypes.POINTER(d), ctypes.POINTER(i), ctypes.POINTER(d)]
+        L.oenv_render_full.argtypes = [vp, vp, vp]
+        L.oenv_get_bodies.restype = i; L.oenv_get_bodies.argtypes = [vp, vp, i]
+        L.oenv_num_arbiters.restype = i; L.oenv_num_arbiters.argtypes = [vp]
+        L.oenv_get_entities.restype = i; L.oenv_get_entities.argtypes = [vp, vp, vp, vp, vp]
+        L.o_mt_seed.argtypes = [vp, u32]
+        L.o_mt_next32.restype = u32; L.o_mt_next32.argtypes = [vp]
+        L.o_mt_double.restype = d; L.o_mt_double.argtypes = [vp]
+        L.o_mt_uniform.restype = d; L.o_mt_uniform.argtypes = [vp, d, d]
+        L.o_mt_randint.restype = ctypes.c_int64; L.o_mt_randint.argtypes = [vp, ctypes.c_int64, ctypes.c_int64]
+        L.o_mt_interval.restype = ctypes.c_uint64; L.o_mt_interval.argtypes = [vp, ctypes.c_uint64]
+        L.o_convex_hull.restype = i; L.o_convex_hull.argtypes = [i, vp, vp, vp, d]
+        L.o_moment_for_poly.restype = d
+        L.o_star_decomposition.restype = i; L.o_star_decomposition.argtypes = [d, d, vp, vp, i]
+        L.o_finger_verts.argtypes = [d, d, d, i, vp, vp]
+        L.o_transform_trs.argtypes = [d, d, d, d, d, vp]
+        L.o_mat3_mul.argtypes = [vp, vp, vp]
+        L.o_allo_view.argtypes = [vp]
+        L.o_ego_view.argtypes = [d, d, d, vp]
+        _lib = L
+    return _lib
+
+
+def ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class MT:
+    """numpy-legacy MT19937 restatement (oracle/rng.c)."""
+
+    def __init__(self, seed):
+        self.buf = np.zeros(625 * 4 + 16, dtype=np.uint8)
+        lib().o_mt_seed(ptr(self.buf), seed)
+
+    def next32(self):
+        return lib().o_mt_next32(ptr(self.buf))
+
+    def double(self):
+        return lib().o_mt_double(ptr(self.buf))
+
+    def uniform(self, lo, hi):
+        return lib().o_mt_uniform(ptr(self.buf), lo, hi)
+
+    def randint(self, lo, hi):
+        return lib().o_mt_randint(ptr(self.buf), lo, hi)
+
+    def interval(self, mx):
+        return lib().o_mt_interval(ptr(self.buf), mx)
+
+
+def star_parts(out_rad, in_rad):
+    out = np.zeros((64, 2))
+    counts = np.zeros(8, dtype=np.int32)
+    n = lib().o_star_decomposition(out_rad, in_rad, ptr(out), ptr(counts), 8)
+    parts, off = [], 0
+    for k in range(n):
+        parts.append(out[off:off + counts[k]].copy())
+        off += counts[k]
+    return parts
+
+
+class OracleEnv:
+    """One reference env (single instance, CPU)."""
+
+    def __init__(self, task, rand_flags, preproc, max_steps, seed=0):
+        self.L = lib()
+        self.h = self.L.oenv_create(TASKS[task] if isinstance(task, str) else task, rand_flags,
+                                    PREPROCS[preproc] if not isinstance(preproc, int) else preproc,
+                                    max_steps, seed)
+        self.nbytes = self.L.oenv_obs_bytes(self.h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.oenv_destroy(self.h)
+            self.h = None
+
+    def seed(self, s):
+        self.L.oenv_seed(self.h, s)
+
+    def reset(self):
+        obs = np.zeros(self.nbytes, dtype=np.uint8)
+        rc = self.L.oenv_reset(self.h, ptr(obs))
+        if rc != 0:
+            raise RuntimeError("oracle table overflow")
+        return obs
+
+    def step(self, action):
+        obs = np.zeros(self.nbytes, dtype=np.uint8)
+        r, dn, sc = ctypes.c_double(), ctypes.c_int(), ctypes.c_double()
+        rc = self.L.oenv_step(self.h, int(action), ptr(obs), ctypes.byref(r), ctypes.byref(dn), ctypes.byref(sc))
+        if rc != 0:
+            raise RuntimeError("oracle table overflow")
+        return obs, r.value, bool(dn.value), sc.value
+
+    def render_full(self):
+        a = np.zeros((384, 384, 3), dtype=np.uint8)
+        g = np.zeros((384, 384, 3), dtype=np.uint8)
+        self.L.oenv_render_full(self.h, ptr(a), ptr(g))
+        return a, g
+
+    def bodies(self):
+        out = np.zeros((32, 6))
+        n = self.L.oenv_get_bodies(self.h, ptr(out), 32)
+        return out[:n].copy()
+
+    def num_arbiters(self):
+        return self.L.oenv_num_arbiters(self.h)
+
+    def entities(self):
+        k = np.zeros(32, dtype=np.int32)
+        t = np.zeros(32, dtype=np.int32)
+        c = np.zeros(32, dtype=np.int32)
+        p = np.zeros((32, 4))
+        n = self.L.oenv_get_entities(self.h, ptr(k), ptr(t), ptr(c), ptr(p))
+        return k[:n].copy(), t[:n].copy(), c[:n].copy(), p[:n].copy()
