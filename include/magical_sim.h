@@ -1,0 +1,87 @@
+/*
+ * magical_sim.h -- C ABI of the MI355X batched MAGICAL simulator.
+ *
+ * Drop-in boundary for the reference hot path:
+ * one mg_sim holds N environment instances of one registered MAGICAL env name
+ * (benchmarks/__init__.py:427-1102) on one GPU.  mg_step replaces, for all N
+ * instances at once, the reference's per-env call chain
+ *     TimeLimit.step -> ResizeDictObservation / FlattenFrameStack /
+ *     EagerDictFrameStack (benchmarks/__init__.py:51-190)
+ *       -> BaseEnv.step (base_env.py:267-307)
+ *            -> Robot.set_action / Robot.update (entities.py:435-476)
+ *            -> pymunk Space.step x 10 (base_env.py:248-255)
+ *            -> score_on_end_of_traj (task files)
+ *            -> BaseEnv.render (base_env.py:324-343, render.py:385-395)
+ * and mg_reset replaces BaseEnv.reset (base_env.py:190-246) + on_reset.
+ *
+ * Conventions: functions return 0 on success or a negative errno-style code;
+ * mg_last_error() returns a thread-local message.  No C++ exception crosses the
+ * ABI.  Output buffers are caller-owned device pointers; the library owns its
+ * internal state and frees it in mg_destroy.  All work is enqueued on the given
+ * HIP stream (hipStream_t passed as void*; NULL = default stream).  One handle
+ * per GPU, used from one host thread.
+ */
+#ifndef MAGICAL_SIM_H
+#define MAGICAL_SIM_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mg_sim mg_sim;
+
+typedef struct {
+    int32_t task;              /* 0 MoveToRegion 1 MoveToCorner 2 ClusterColour 3 ClusterShape 4 MatchRegions */
+    int32_t rand_flags;        /* bit 0 layout minor, 1 layout full, 2 colour, 3 shape type, 4 count, 5 dynamics */
+    int32_t preproc;           /* 0 none, 1 LoRes4E, 2 LoResStack, 4 LoRes4A */
+    int32_t num_envs;
+    int32_t device;            /* HIP device ordinal */
+    int32_t max_episode_steps; /* TimeLimit / BaseEnv.max_episode_steps */
+    uint32_t base_seed;        /* env i seeded base_seed + i when seeds == NULL */
+    int32_t auto_reset;        /* 1: finished episodes reset inside mg_step (VecEnv); 0: gym single-env semantics */
+    const uint32_t *seeds;     /* host array [num_envs] or NULL */
+    const void *library;       /* host pointer to an mg_library (layout: magical-1_amd/csrc/mg_common.h,
+                                  built by magical_amd.tables from the reference formulas) */
+    int64_t library_size;      /* sizeof(mg_library), checked */
+} mg_config;
+
+typedef struct {
+    uint8_t *obs_allo;   /* LoRes4E/4A: u8[N,96,96,3]; LoResStack: u8[N,96,96,12] */
+    uint8_t *obs_ego;    /* same shapes as obs_allo */
+    uint8_t *obs_past;   /* LoRes4E/4A: u8[N,96,96,12]; NULL otherwise */
+    float *reward;       /* f32[N] (eval_score at done, else 0) */
+    uint8_t *done;       /* u8[N] */
+    double *eval_score;  /* f64[N] (info['eval_score']) */
+} mg_buffers;
+
+/* replaces gym.make(name) for N instances (benchmarks/__init__.py:232-266) */
+int mg_create(const mg_config *cfg, mg_sim **out);
+/* caller-owned output buffers (device pointers) */
+int mg_bind_outputs(mg_sim *sim, const mg_buffers *buf);
+/* BaseEnv.reset for every env (mask == NULL) or envs with mask[i] != 0 (device u8[N]);
+ * writes the LoRes observation of the reset envs */
+int mg_reset(mg_sim *sim, const uint8_t *mask_dev, void *stream);
+/* BaseEnv.step for all envs; actions: device u8[N] in [0, 18); envs that reach
+ * max_episode_steps report done/reward/eval_score and are reset in place
+ * (their observation is the first frame of the next episode) */
+int mg_step(mg_sim *sim, const uint8_t *actions_dev, void *stream);
+/* BaseEnv.render('rgb_array') of every env: device u8[N,2,384,384,3] (allo, ego) */
+int mg_render_full(mg_sim *sim, uint8_t *out_dev, void *stream);
+/* parity dumps: per env per body slot (px, py, angle, vx, vy, w): device f64[N,16,6];
+ * counts: device i32[N,4] = (bodies, shapes, constraints, active arbiters) */
+int mg_get_bodies(mg_sim *sim, double *out_dev, int32_t *counts_dev, void *stream);
+/* per-env error flags (table overflow, placement failure, raster assumption): device i32[N] */
+int mg_get_errors(mg_sim *sim, int32_t *out_dev, void *stream);
+/* re-seed env RNGs (env.seed): host u32[num_envs] */
+int mg_seed(mg_sim *sim, const uint32_t *seeds_host);
+/* device-side uniform random actions for throughput runs (Philox 4x32-10, key, counter = (step, env)) */
+int mg_random_actions(mg_sim *sim, uint8_t *actions_dev, uint64_t key, uint64_t step, void *stream);
+int mg_num_envs(const mg_sim *sim);
+void mg_destroy(mg_sim *sim);
+const char *mg_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

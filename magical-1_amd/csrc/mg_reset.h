@@ -1,0 +1,483 @@
+// mg_reset.h -- per-lane episode reset: task on_reset, entity setup, randomisers.
+//
+// base_env.py:190-246 (reset: new Space, PhysicsVariables.sample, arena,
+// on_reset), entities.py:238-433 / 580-754 / 762-801 (entity setup),
+// geom.py:116-384 (pm_randomise_pose rejection sampling with shape queries,
+// pm_randomise_all_poses, randomise_hw, pm_shift_bodies), task files
+// move_to_region.py:30-83, move_to_corner.py:125-159, cluster.py:67-164,
+// match_regions.py:44-191.  RNG: numpy legacy RandomState (MT19937) per env,
+// drawn in the reference's order so parity mode replays the reference stream.
+#pragma once
+#include "mg_step.h"
+
+#define MT(i) S.mt_key[(size_t)(i) * (size_t)S.N + (size_t)e]
+
+MG_DEV void mt_seed(const MGState &S, int e, uint32_t seed) {
+    uint32_t v = seed;
+    for (int i = 0; i < 624; i++) {
+        MT(i) = v;
+        v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)(i + 1);
+    }
+    S.mt_pos[e] = 624;
+}
+MG_DEV uint32_t mt_next32(const MGState &S, int e) {
+    int pos = S.mt_pos[e];
+    if (pos == 624) {
+        const uint32_t UPPER = 0x80000000u, LOWER = 0x7fffffffu, MA = 0x9908b0dfu;
+        uint32_t y;
+        int i;
+        for (i = 0; i < 624 - 397; i++) {
+            y = (MT(i) & UPPER) | (MT(i + 1) & LOWER);
+            MT(i) = MT(i + 397) ^ (y >> 1) ^ (-(y & 1u) & MA);
+        }
+        for (; i < 623; i++) {
+            y = (MT(i) & UPPER) | (MT(i + 1) & LOWER);
+            MT(i) = MT(i - 227) ^ (y >> 1) ^ (-(y & 1u) & MA);
+        }
+        y = (MT(623) & UPPER) | (MT(0) & LOWER);
+        MT(623) = MT(396) ^ (y >> 1) ^ (-(y & 1u) & MA);
+        pos = 0;
+    }
+    uint32_t y = MT(pos);
+    S.mt_pos[e] = pos + 1;
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+MG_DEV double mt_double(const MGState &S, int e) {
+    int32_t a = (int32_t)(mt_next32(S, e) >> 5);
+    int32_t b = (int32_t)(mt_next32(S, e) >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+MG_DEV double mt_uniform(const MGState &S, int e, double lo, double hi) {
+    double range = hi - lo;
+    return lo + range * mt_double(S, e);
+}
+MG_DEV uint32_t mt_masked(const MGState &S, int e, uint32_t rng) { // uniform in [0, rng]
+    if (rng == 0) return 0;
+    uint32_t m = rng;
+    m |= m >> 1; m |= m >> 2; m |= m >> 4; m |= m >> 8; m |= m >> 16;
+    uint32_t v;
+    while ((v = (mt_next32(S, e) & m)) > rng) {}
+    return v;
+}
+MG_DEV int mt_randint(const MGState &S, int e, int lo, int hi) { return lo + (int)mt_masked(S, e, (uint32_t)(hi - 1 - lo)); }
+
+// ---- entity instantiation -------------------------------------------------
+struct Builder { int nb, ns, nc, hash; };
+
+MG_DEV int add_body(const MGState &S, int e, Builder &B, bool kin, double m, double i, double px, double py, double a) {
+    int b = B.nb++;
+    AT(S.bkin, b) = kin ? 1 : 0;
+    AT(S.bminv, b) = kin ? 0.0 : 1.0 / m;
+    AT(S.biinv, b) = kin ? 0.0 : 1.0 / i;
+    AT(S.bpx, b) = px; AT(S.bpy, b) = py;
+    AT(S.bvx, b) = 0.0; AT(S.bvy, b) = 0.0; AT(S.bw, b) = 0.0;
+    AT(S.bvbx, b) = 0.0; AT(S.bvby, b) = 0.0; AT(S.bwb, b) = 0.0;
+    AT(S.bacache, b) = NAN;
+    body_set_angle(S, e, b, a);
+    return b;
+}
+MG_DEV int add_shape(const MGState &S, int e, Builder &B, int body, int poly, double r, double u, int group, int ent) {
+    int k = B.ns++;
+    AT(S.sbody, k) = (int8_t)body; AT(S.spoly, k) = (int8_t)poly; AT(S.sent, k) = (int8_t)ent;
+    AT(S.sgroup, k) = (int16_t)group; AT(S.shash, k) = (int16_t)(B.hash++);
+    AT(S.scat, k) = 1; AT(S.sr, k) = r; AT(S.su, k) = u;
+    return k;
+}
+MG_DEV int add_cons(const MGState &S, int e, Builder &B, int type, int a, int b, double maxF, double maxB, double bcoef) {
+    int c = B.nc++;
+    AT(S.ctype, c) = (int8_t)type; AT(S.ca, c) = (int8_t)a; AT(S.cb, c) = (int8_t)b;
+    for (int k = 0; k < CP_NUM; k++) CPA(k, c) = 0.0;
+    CPA(CP_MAXF, c) = maxF; CPA(CP_MAXB, c) = maxB; CPA(CP_BCOEF, c) = bcoef;
+    return c;
+}
+
+// cpBodyWorldToLocal via cpTransformRigidInverse
+MG_DEV V2 world_to_local(const MGState &S, int e, int b, V2 pt) {
+    double c = AT(S.brc, b), s = AT(S.brs, b), tx = AT(S.bpx, b), ty = AT(S.bpy, b);
+    double ta = c, tb = s, tc = -s, td = c;
+    double ia = td, ic = -tc, itx = tc * ty - tx * td;
+    double ib = -tb, id = ta, ity = tx * tb - ta * ty;
+    return v2(ia * pt.x + ic * pt.y + itx, ib * pt.x + id * pt.y + ity);
+}
+
+MG_DEV V2 rotated(V2 v, double ang) {
+    double s, c;
+    mg_sincos(ang, s, c);
+    return v2(v.x * c - v.y * s, v.x * s + v.y * c);
+}
+
+MG_DEV void add_robot(const MGState &S, const mg_library *L, int e, Builder &B, int ent, double px, double py, double ang) {
+    const double *pv = S.pv;
+    size_t N = (size_t)S.N;
+    double radius = L->robot_radius;
+    int body = add_body(S, e, B, false, L->robot_mass, L->robot_inertia, px, py, ang);
+    int control = add_body(S, e, B, true, 0, 0, px, py, ang);
+    S.robot_body0[e] = body;
+    S.robot_cons0[e] = B.nc;
+    int c = add_cons(S, e, B, MG_C_PIVOT, control, body, pv[0 * N + e], 0.0, L->default_bias_coef);
+    c = add_cons(S, e, B, MG_C_GEAR, control, body, pv[1 * N + e], 2.5, 1.0);
+    CPA(CP_PHASE, c) = 0.0; CPA(CP_RATIO, c) = 1.0; CPA(CP_RATIO_INV, c) = 1.0 / 1.0;
+    for (int k = 0; k < 2; k++) {
+        int eye = add_body(S, e, B, false, L->eye_mass, L->eye_inertia, 0.0, 0.0, ang);
+        c = add_cons(S, e, B, MG_C_SPRING, body, eye, 0.001, 3.0, L->default_bias_coef);
+        CPA(CP_REST, c) = 0.0; CPA(CP_STIFF, c) = 0.1; CPA(CP_WCOEF, c) = L->spring_w_coef;
+    }
+    int fingers[2];
+    for (int k = 0; k < 2; k++) {
+        V2 rel = v2(L->finger_rel[k][0], L->finger_rel[k][1]);
+        V2 relr = rotated(rel, ang);
+        V2 fp = v2(AT(S.bpx, body) + relr.x, AT(S.bpy, body) + relr.y);
+        int fb = add_body(S, e, B, false, L->finger_mass, L->finger_inertia[k], fp.x, fp.y, ang + L->finger_angle_off[k]);
+        fingers[k] = fb;
+        V2 pivot = v2(AT(S.bpx, fb), AT(S.bpy, fb));
+        V2 aa = world_to_local(S, e, body, pivot), ab = world_to_local(S, e, fb, pivot);
+        c = add_cons(S, e, B, MG_C_PIVOT, body, fb, INFINITY, INFINITY, 1.0);
+        CPA(CP_AAX, c) = aa.x; CPA(CP_AAY, c) = aa.y; CPA(CP_ABX, c) = ab.x; CPA(CP_ABY, c) = ab.y;
+        c = add_cons(S, e, B, MG_C_ROTLIMIT, body, fb, INFINITY, INFINITY, 1.0);
+        CPA(CP_MIN, c) = L->finger_lim[k][0]; CPA(CP_MAX, c) = L->finger_lim[k][1];
+        c = add_cons(S, e, B, MG_C_MOTOR, body, fb, pv[2 * N + e], 0.0, L->default_bias_coef);
+        CPA(CP_RATE, c) = 0.0;
+    }
+    add_shape(S, e, B, body, -1, radius, 0.5, 1, ent);
+    for (int k = 0; k < 2; k++)
+        for (int p = 0; p < 2; p++) {
+            int poly = L->finger_poly[2 * k + p];
+            add_shape(S, e, B, fingers[k], poly, L->poly_r[poly], 5.0, 1, ent);
+        }
+}
+
+MG_DEV void add_block(const MGState &S, const mg_library *L, int e, Builder &B, int ent, int type, double px, double py,
+                      double ang, int star_group) {
+    size_t N = (size_t)S.N;
+    int body = add_body(S, e, B, false, L->block_mass[type], L->block_inertia[type], px, py, ang);
+    int group = type == MG_SHAPE_STAR ? star_group : 0;
+    for (int i = 0; i < L->block_nshapes[type]; i++) {
+        int poly = L->block_poly[type][i];
+        double r = poly < 0 ? L->block_circle_r : L->poly_r[poly];
+        add_shape(S, e, B, body, poly, r, 0.5, group, ent);
+    }
+    int c = add_cons(S, e, B, MG_C_PIVOT, -1, body, S.pv[3 * N + e], 0.0, L->default_bias_coef);
+    c = add_cons(S, e, B, MG_C_GEAR, -1, body, S.pv[4 * N + e], 0.0, L->default_bias_coef);
+    CPA(CP_PHASE, c) = 0.0; CPA(CP_RATIO, c) = 1.0; CPA(CP_RATIO_INV, c) = 1.0 / 1.0;
+}
+
+// ---- shape queries (cpSpaceShapeQuery semantics, sensors reported) --------
+MG_DEV bool query_hits(const MGState &S, const mg_library *L, int e, const ShapeW &A, int self_k, int group, bool has_goal,
+                       bool self_is_goal) {
+    for (int w = 0; w < 4; w++) {
+        ShapeW W;
+        load_wall(w, W);
+        if (!bb_intersects(A, W)) continue;
+        Collision info;
+        collide(A, W, info);
+        if (info.count) return true;
+    }
+    if (has_goal && !self_is_goal) {
+        int ge = S.goal_ent[e];
+        if (AT(S.eshape0, ge) != 0) { // goal enabled (categories != 0)
+            ShapeW G;
+            load_goal(S.gpx[e], S.gpy[e], AT(S.ew, ge), AT(S.eh, ge), 0, G);
+            if (bb_intersects(A, G)) {
+                Collision info;
+                collide(A, G, info);
+                if (info.count) return true;
+            }
+        }
+    }
+    int ns = S.nshapes[e];
+    for (int j = 0; j < ns; j++) {
+        if (j == self_k || !AT(S.scat, j)) continue;
+        int gj = AT(S.sgroup, j);
+        if (group != 0 && group == gj) continue;
+        ShapeW O;
+        load_shape(S, L, e, j, 0, O);
+        if (!bb_intersects(A, O)) continue;
+        Collision info;
+        collide(A, O, info);
+        if (info.count) return true;
+    }
+    return false;
+}
+
+MG_DEV void ent_set_enabled(const MGState &S, int e, int ent, int on) {
+    if (AT(S.ekind, ent) == MG_ENT_GOAL) { AT(S.eshape0, ent) = (int8_t)on; return; }
+    int s0 = AT(S.eshape0, ent), n = AT(S.enshapes, ent);
+    for (int k = s0; k < s0 + n; k++) AT(S.scat, k) = (uint8_t)on;
+}
+
+// pm_shift_bodies (geom.py:362-384)
+MG_DEV void shift_entity(const MGState &S, int e, int ent, V2 pos, double ang) {
+    if (AT(S.ekind, ent) == MG_ENT_GOAL) {
+        V2 root = v2(S.gpx[e], S.gpy[e]);
+        V2 d = v2(S.gpx[e] - root.x, S.gpy[e] - root.y);
+        V2 r = rotated(d, ang - 0.0);
+        S.gpx[e] = pos.x + r.x; S.gpy[e] = pos.y + r.y;
+        return;
+    }
+    int b0 = AT(S.ebody0, ent);
+    int nb = AT(S.ekind, ent) == MG_ENT_ROBOT ? 6 : 1;
+    double root_a = AT(S.ba, b0);
+    V2 root_p = v2(AT(S.bpx, b0), AT(S.bpy, b0));
+    for (int b = b0; b < b0 + nb; b++) {
+        double lad = AT(S.ba, b) - root_a;
+        V2 lpd = v2(AT(S.bpx, b) - root_p.x, AT(S.bpy, b) - root_p.y);
+        body_set_angle(S, e, b, ang + lad);
+        V2 r = rotated(lpd, ang - root_a);
+        // cpBodySetPosition: p = T(cog = 0) + position
+        double c = AT(S.brc, b), s = AT(S.brs, b);
+        V2 t0 = v2(c * 0.0 + (-s) * 0.0, s * 0.0 + c * 0.0);
+        AT(S.bpx, b) = t0.x + (pos.x + r.x);
+        AT(S.bpy, b) = t0.y + (pos.y + r.y);
+    }
+}
+
+MG_DEV bool entity_collides(const MGState &S, const mg_library *L, int e, int ent) {
+    bool has_goal = S.goal_ent[e] >= 0;
+    if (AT(S.ekind, ent) == MG_ENT_GOAL) {
+        ShapeW G;
+        load_goal(S.gpx[e], S.gpy[e], AT(S.ew, ent), AT(S.eh, ent), 0, G);
+        return query_hits(S, L, e, G, -1, 0, has_goal, true);
+    }
+    int s0 = AT(S.eshape0, ent), n = AT(S.enshapes, ent);
+    for (int k = s0; k < s0 + n; k++) {
+        ShapeW A;
+        load_shape(S, L, e, k, 0, A);
+        if (query_hits(S, L, e, A, k, AT(S.sgroup, k), has_goal, false)) return true;
+    }
+    return false;
+}
+
+// pm_randomise_pose (geom.py:116-264); pos_limit / rot_limit < 0 mean None
+MG_DEV int randomise_pose(const MGState &S, const mg_library *L, int e, int ent, bool rand_rot, double pos_limit,
+                          double rot_limit) {
+    bool goal = AT(S.ekind, ent) == MG_ENT_GOAL;
+    int b0 = goal ? -1 : AT(S.ebody0, ent);
+    double orig_a = goal ? 0.0 : AT(S.ba, b0);
+    V2 orig_p = goal ? v2(S.gpx[e], S.gpy[e]) : v2(AT(S.bpx, b0), AT(S.bpy, b0));
+    double xlo = -1, xhi = 1, ylo = -1, yhi = 1;
+    if (pos_limit >= 0) {
+        xlo = fmax(-1.0, orig_p.x - pos_limit); xhi = fmin(1.0, orig_p.x + pos_limit);
+        ylo = fmax(-1.0, orig_p.y - pos_limit); yhi = fmin(1.0, orig_p.y + pos_limit);
+    }
+    double rmin = -3.141592653589793, rmax = 3.141592653589793;
+    if (rot_limit >= 0) { rmin = orig_a - rot_limit; rmax = orig_a + rot_limit; }
+    for (int tries = 0; tries < 10000; tries++) {
+        double x = mt_uniform(S, e, xlo, xhi);
+        double y = mt_uniform(S, e, ylo, yhi);
+        double a = rand_rot ? mt_uniform(S, e, rmin, rmax) : orig_a;
+        shift_entity(S, e, ent, v2(x, y), a);
+        if (!entity_collides(S, L, e, ent)) return 0;
+    }
+    shift_entity(S, e, ent, orig_p, orig_a);
+    return -1;
+}
+
+MG_DEV void randomise_all(const MGState &S, const mg_library *L, int e, const int *ents, int n, const bool *rand_rot,
+                          double pos_limit, const double *rot_limits) {
+    for (int retry = 0; retry < 10; retry++) {
+        for (int k = 0; k < n; k++) ent_set_enabled(S, e, ents[k], 0);
+        bool failed = false;
+        for (int k = 0; k < n && !failed; k++) {
+            ent_set_enabled(S, e, ents[k], 1);
+            if (randomise_pose(S, L, e, ents[k], rand_rot[k], pos_limit, rot_limits[k]) != 0) failed = true;
+        }
+        if (!failed) return;
+    }
+    S.overflow[e] |= 2; // PlacementError after 10 retries
+}
+
+// ---- tasks -----------------------------------------------------------------
+struct TaskCfg { int task, flags; };
+__constant__ static const int MG_SHAPE_COLOURS[4] = {MG_COL_RED, MG_COL_GREEN, MG_COL_BLUE, MG_COL_YELLOW};
+__constant__ static const int MG_SHAPE_TYPES[4] = {MG_SHAPE_SQUARE, MG_SHAPE_PENTAGON, MG_SHAPE_STAR, MG_SHAPE_CIRCLE};
+
+MG_DEV int new_entity(const MGState &S, int e, int kind, int type, int colour, int role, double x, double y, double a) {
+    int i = S.nents[e]++;
+    AT(S.ekind, i) = (int8_t)kind; AT(S.etype, i) = (int8_t)type; AT(S.ecol, i) = (int8_t)colour;
+    AT(S.erole, i) = (int8_t)role;
+    AT(S.ex, i) = x; AT(S.ey, i) = y; AT(S.eang, i) = a; AT(S.eh, i) = 0.0; AT(S.ew, i) = 0.0;
+    AT(S.ebody0, i) = 0; AT(S.eshape0, i) = 0; AT(S.enshapes, i) = 0;
+    return i;
+}
+
+MG_DEV void inst_robot(const MGState &S, const mg_library *L, int e, Builder &B, double x, double y, double a) {
+    int ent = new_entity(S, e, MG_ENT_ROBOT, 0, MG_COL_GREY, 0, x, y, a);
+    AT(S.ebody0, ent) = (int8_t)B.nb; AT(S.eshape0, ent) = (int8_t)B.ns;
+    add_robot(S, L, e, B, ent, x, y, a);
+    AT(S.enshapes, ent) = (int8_t)(B.ns - AT(S.eshape0, ent));
+}
+MG_DEV void inst_block(const MGState &S, const mg_library *L, int e, Builder &B, int type, int colour, int role, double x,
+                       double y, double a, int &star_groups) {
+    int ent = new_entity(S, e, MG_ENT_BLOCK, type, colour, role, x, y, a);
+    AT(S.ebody0, ent) = (int8_t)B.nb; AT(S.eshape0, ent) = (int8_t)B.ns;
+    int group = 0;
+    if (type == MG_SHAPE_STAR) group = 1000 + (++star_groups);
+    add_block(S, L, e, B, ent, type, x, y, a, group);
+    AT(S.enshapes, ent) = (int8_t)(B.ns - AT(S.eshape0, ent));
+}
+MG_DEV void inst_goal(const MGState &S, int e, Builder &B, double x, double y, double h, double w, int colour) {
+    int ent = new_entity(S, e, MG_ENT_GOAL, 0, colour, 0, x, y, 0.0);
+    AT(S.eh, ent) = h; AT(S.ew, ent) = w;
+    AT(S.eshape0, ent) = 1; // enabled flag for goals
+    S.gpx[e] = x + w / 2; S.gpy[e] = y - h / 2;
+    S.goal_ent[e] = ent;
+    B.hash++;
+}
+
+#define JITTER_POS_BOUND (1 * 0.05 / 2.0)
+#define JITTER_ROT_BOUND (0.05 * 3.141592653589793)
+#define JITTER_TARGET_BOUND (0.05 * (0.8 - 0.5) / 2)
+
+MG_DEV void randomise_hw(const MGState &S, int e, double ch, double cw, double linf, double &h, double &w) {
+    double lo0 = 0.5, lo1 = 0.5, hi0 = 0.8, hi1 = 0.8;
+    if (linf >= 0) {
+        lo0 = fmax(lo0, ch - linf); lo1 = fmax(lo1, cw - linf);
+        hi0 = fmin(hi0, ch + linf); hi1 = fmin(hi1, cw + linf);
+    }
+    h = mt_uniform(S, e, lo0, hi0);
+    w = mt_uniform(S, e, lo1, hi1);
+}
+
+__constant__ static const int CC_COLOURS[2][8] = {
+    {MG_COL_BLUE, MG_COL_BLUE, MG_COL_BLUE, MG_COL_GREEN, MG_COL_GREEN, MG_COL_RED, MG_COL_YELLOW, MG_COL_YELLOW},
+    {MG_COL_YELLOW, MG_COL_BLUE, MG_COL_RED, MG_COL_RED, MG_COL_GREEN, MG_COL_YELLOW, MG_COL_BLUE, MG_COL_GREEN}};
+__constant__ static const int CC_TYPES[2][8] = {
+    {MG_SHAPE_CIRCLE, MG_SHAPE_STAR, MG_SHAPE_SQUARE, MG_SHAPE_PENTAGON, MG_SHAPE_PENTAGON, MG_SHAPE_SQUARE, MG_SHAPE_STAR,
+     MG_SHAPE_PENTAGON},
+    {MG_SHAPE_SQUARE, MG_SHAPE_PENTAGON, MG_SHAPE_PENTAGON, MG_SHAPE_PENTAGON, MG_SHAPE_CIRCLE, MG_SHAPE_STAR, MG_SHAPE_STAR,
+     MG_SHAPE_CIRCLE}};
+__constant__ static const double CC_POSES[2][8][3] = {
+    {{-0.5147, 0.14149, -0.38871}, {-0.1347, -0.71414, 1.0533}, {-0.74247, -0.097592, 1.1571},
+     {-0.077363, -0.42964, -0.64379}, {0.51978, 0.1853, -1.1762}, {-0.5278, -0.21642, 2.9356},
+     {-0.54039, 0.48292, 0.072818}, {-0.16761, 0.64303, -2.3255}},
+    {{-0.414, 0.297, -1.731}, {0.068, 0.705, 2.184}, {0.821, 0.220, 0.650}, {-0.461, -0.749, -2.673},
+     {0.867, -0.149, -2.215}, {-0.785, -0.140, -0.405}, {-0.305, -0.226, 1.341}, {0.758, -0.708, -2.140}}};
+__constant__ static const double CC_ROBOT[2][3] = {{0.71692, -0.34374, 0.83693}, {0.286, -0.202, -1.878}};
+
+MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg) {
+    size_t N = (size_t)S.N;
+    const int f = cfg.flags;
+    S.episode_steps[e] = 0;
+    for (int i = 0; i < MG_MAX_ARB; i++) { AT(S.akey, i) = -1; AT(S.acount, i) = 0; AT(S.astate, i) = ARB_FIRST; }
+    S.nactive[e] = 0; S.stamp[e] = 0; S.curr_dt[e] = 0.0; S.nents[e] = 0; S.goal_ent[e] = -1;
+    S.target_speed[e] = 0.0; S.rel_turn[e] = 0.0; S.target_finger[e] = 0.0;
+    const double PV_DEF[5] = {3, 1, 4, 1.5, 0.1}, PV_LO[5] = {2.2, 0.7, 2.5, 1.0, 0.07}, PV_HI[5] = {3.5, 1.5, 4.5, 1.8, 0.15};
+    for (int i = 0; i < 5; i++)
+        S.pv[i * N + e] = (f & MG_RAND_DYNAMICS) ? mt_uniform(S, e, PV_LO[i], PV_HI[i]) : PV_DEF[i];
+    Builder B = {0, 0, 0, 4}; // arena segments hold hashids 0..3
+    new_entity(S, e, MG_ENT_ARENA, 0, MG_COL_GREY, 0, 0, 0, 0);
+    int star_groups = 0;
+    const bool any_layout = (f & (MG_RAND_LAYOUT_MINOR | MG_RAND_LAYOUT_FULL)) != 0;
+    const bool minor = (f & MG_RAND_LAYOUT_MINOR) != 0;
+    int ents[16]; bool rr[16]; double rl[16]; int n = 0;
+    if (cfg.task == MG_TASK_MOVE_TO_REGION) {
+        double gx = -0.62, gy = -0.17, gh = 0.76, gw = 0.75;
+        if (any_layout) randomise_hw(S, e, gh, gw, minor ? JITTER_TARGET_BOUND : -1.0, gh, gw);
+        int colour = MG_COL_BLUE;
+        if (f & MG_RAND_COLOUR) colour = MG_SHAPE_COLOURS[mt_randint(S, e, 0, 4)];
+        inst_goal(S, e, B, gx, gy, gh, gw, colour);
+        inst_robot(S, L, e, B, 0.058, 0.53, -2.13);
+        if (any_layout) {
+            ents[0] = 1; ents[1] = 2; rr[0] = false; rr[1] = true;
+            rl[0] = -1; rl[1] = minor ? JITTER_ROT_BOUND : -1;
+            n = 2;
+            S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
+            randomise_all(S, L, e, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl);
+        }
+    } else if (cfg.task == MG_TASK_MOVE_TO_CORNER) {
+        double rx = mt_double(S, e), ry = mt_double(S, e);
+        inst_robot(S, L, e, B, rx, ry, 0.55 * 3.141592653589793);
+        int colour = MG_COL_RED, type = MG_SHAPE_SQUARE;
+        if (f & MG_RAND_COLOUR) colour = MG_SHAPE_COLOURS[mt_randint(S, e, 0, 4)];
+        if (f & MG_RAND_SHAPE_TYPE) type = MG_SHAPE_TYPES[mt_randint(S, e, 0, 4)];
+        inst_block(S, L, e, B, type, colour, 0, 0.1, -0.65, 0.13 * 3.141592653589793, star_groups);
+        if (minor) {
+            ents[0] = 1; ents[1] = 2; rr[0] = rr[1] = true; rl[0] = rl[1] = JITTER_ROT_BOUND; n = 2;
+            S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
+            randomise_all(S, L, e, ents, n, rr, JITTER_POS_BOUND, rl);
+        }
+    } else if (cfg.task == MG_TASK_CLUSTER_COLOUR || cfg.task == MG_TASK_CLUSTER_SHAPE) {
+        int by = cfg.task == MG_TASK_CLUSTER_SHAPE ? 1 : 0;
+        int nblk = 8;
+        bool count = (f & MG_RAND_SHAPE_COUNT) != 0;
+        if (count) nblk = mt_randint(S, e, 7, 10 + 1);
+        int cols[10], types[10];
+        if (f & MG_RAND_COLOUR) {
+            for (int i = 0; i < 4; i++) cols[i] = MG_SHAPE_COLOURS[i];
+            for (int i = 4; i < nblk; i++) cols[i] = MG_SHAPE_COLOURS[mt_randint(S, e, 0, 4)];
+            for (int i = nblk - 1; i >= 1; i--) { int j = (int)mt_masked(S, e, (uint32_t)i); int t = cols[i]; cols[i] = cols[j]; cols[j] = t; }
+        } else for (int i = 0; i < 8; i++) cols[i] = CC_COLOURS[by][i];
+        if (f & MG_RAND_SHAPE_TYPE) {
+            for (int i = 0; i < 4; i++) types[i] = MG_SHAPE_TYPES[i];
+            for (int i = 4; i < nblk; i++) types[i] = MG_SHAPE_TYPES[mt_randint(S, e, 0, 4)];
+            for (int i = nblk - 1; i >= 1; i--) { int j = (int)mt_masked(S, e, (uint32_t)i); int t = types[i]; types[i] = types[j]; types[j] = t; }
+        } else for (int i = 0; i < 8; i++) types[i] = CC_TYPES[by][i];
+        for (int i = 0; i < nblk; i++) {
+            double x = count ? 0.0 : CC_POSES[by][i][0], y = count ? 0.0 : CC_POSES[by][i][1], a = count ? 0.0 : CC_POSES[by][i][2];
+            inst_block(S, L, e, B, types[i], cols[i], 0, x, y, a, star_groups);
+        }
+        inst_robot(S, L, e, B, CC_ROBOT[by][0], CC_ROBOT[by][1], CC_ROBOT[by][2]);
+        if (any_layout) {
+            bool full = (f & MG_RAND_LAYOUT_FULL) != 0;
+            ents[0] = 1 + nblk;
+            for (int i = 0; i < nblk; i++) ents[1 + i] = 1 + i;
+            n = nblk + 1;
+            for (int i = 0; i < n; i++) { rr[i] = true; rl[i] = full ? -1.0 : JITTER_ROT_BOUND; }
+            S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
+            randomise_all(S, L, e, ents, n, rr, full ? -1.0 : JITTER_POS_BOUND, rl);
+        }
+    } else { // MatchRegions
+        int target = MG_COL_GREEN;
+        if (f & MG_RAND_COLOUR) target = MG_SHAPE_COLOURS[mt_randint(S, e, 0, 4)];
+        int dcols[3], nd = 0;
+        for (int i = 0; i < 4; i++) if (MG_SHAPE_COLOURS[i] != target) dcols[nd++] = MG_SHAPE_COLOURS[i];
+        double th = 0.7, tw = 0.6;
+        if (any_layout) randomise_hw(S, e, th, tw, minor ? JITTER_TARGET_BOUND : -1.0, th, tw);
+        inst_goal(S, e, B, 0.1, 0.7, th, tw, target);
+        const int dtt[2] = {MG_SHAPE_STAR, MG_SHAPE_SQUARE};
+        const int ddt[3][2] = {{0, 0}, {MG_SHAPE_PENTAGON, 0}, {MG_SHAPE_CIRCLE, MG_SHAPE_PENTAGON}};
+        const double dtp[2][3] = {{0.8, -0.7, 2.37}, {-0.68, 0.72, 1.28}};
+        const double ddp[3][2][3] = {{{0, 0, 0}, {0, 0, 0}}, {{-0.05, -0.2, -1.09}, {0, 0, 0}},
+                                     {{-0.75, -0.55, 2.78}, {0.3, -0.82, -1.15}}};
+        int tcount = 2, dcount[3] = {0, 1, 2};
+        if (f & MG_RAND_SHAPE_COUNT) {
+            tcount = mt_randint(S, e, 1, 3);
+            for (int i = 0; i < 3; i++) dcount[i] = mt_randint(S, e, 0, 3);
+        }
+        int ttypes[2], dtypes[3][2];
+        if (f & MG_RAND_SHAPE_TYPE) {
+            for (int i = 0; i < tcount; i++) ttypes[i] = MG_SHAPE_TYPES[mt_randint(S, e, 0, 4)];
+            for (int c = 0; c < 3; c++)
+                for (int i = 0; i < dcount[c]; i++) dtypes[c][i] = MG_SHAPE_TYPES[mt_randint(S, e, 0, 4)];
+        } else {
+            ttypes[0] = dtt[0]; ttypes[1] = dtt[1];
+            for (int c = 0; c < 3; c++) { dtypes[c][0] = ddt[c][0]; dtypes[c][1] = ddt[c][1]; }
+        }
+        bool full = (f & MG_RAND_LAYOUT_FULL) != 0;
+        int first = S.nents[e];
+        for (int i = 0; i < tcount; i++)
+            inst_block(S, L, e, B, ttypes[i], target, 1, full ? 0.0 : dtp[i][0], full ? 0.0 : dtp[i][1], full ? 0.0 : dtp[i][2],
+                       star_groups);
+        for (int c = 0; c < 3; c++)
+            for (int i = 0; i < dcount[c]; i++)
+                inst_block(S, L, e, B, dtypes[c][i], dcols[c], 2, full ? 0.0 : ddp[c][i][0], full ? 0.0 : ddp[c][i][1],
+                           full ? 0.0 : ddp[c][i][2], star_groups);
+        int nblk = S.nents[e] - first;
+        inst_robot(S, L, e, B, -0.5, 0.1, -3.141592653589793 * 1.2);
+        if (any_layout) {
+            n = 0;
+            ents[n++] = 1;                 // sensor
+            ents[n++] = S.nents[e] - 1;    // robot
+            for (int i = 0; i < nblk; i++) ents[n++] = first + i;
+            for (int i = 0; i < n; i++) { rr[i] = i != 0; rl[i] = minor ? JITTER_ROT_BOUND : -1.0; }
+            S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
+            randomise_all(S, L, e, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl);
+        }
+    }
+    S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
+    for (int k = 0; k < B.ns; k++) AT(S.scat, k) = 1;
+}

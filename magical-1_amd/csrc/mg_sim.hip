@@ -1,0 +1,319 @@
+// mg_sim.hip -- gfx950 kernels and the C ABI (include/magical_sim.h).
+//
+// Per env-step (mg_step): step_kernel (one env per lane: action decode,
+// 10 x [Robot.update + cpSpaceStep], episode counter, score, in-place reset
+// of finished episodes) then render_kernel (one workgroup per (env, view):
+// 384^2 raster in LDS bands -> 96^2 area downsample -> LoRes frame stack).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstring>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../../include/magical_sim.h"
+#include "mg_render.h"
+#include "mg_score.h"
+
+static thread_local std::string g_err;
+static int set_err(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+#define HIPC(x)                                                                                        \
+    do {                                                                                               \
+        hipError_t _e = (x);                                                                           \
+        if (_e != hipSuccess) return set_err(-5, std::string(#x) + ": " + hipGetErrorString(_e));      \
+    } while (0)
+
+struct mg_sim {
+    MGState S;
+    mg_library *dlib;
+    void *pool;
+    size_t pool_bytes;
+    int task, flags, preproc, max_steps, device, auto_reset;
+    mg_buffers out;
+    int bound;
+};
+
+// ---------------------------------------------------------------------------
+// kernels
+__global__ void __launch_bounds__(64) seed_kernel(MGState S, const uint32_t *__restrict__ seeds) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= S.n_envs) return;
+    mt_seed(S, e, seeds[e]);
+}
+
+__global__ void __launch_bounds__(64) reset_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg,
+                                                   const uint8_t *__restrict__ mask) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= S.n_envs) return;
+    if (mask && !mask[e]) return;
+    reset_env(S, L, e, cfg);
+}
+
+__global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg, int max_steps,
+                                                  int auto_reset, const uint8_t *__restrict__ actions, float *reward,
+                                                  uint8_t *done, double *eval_score) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= S.n_envs) return;
+    int a = actions[e];
+    robot_set_action(S, L, e, a < 18 ? a : 0);
+    const double dt = L->dt;
+    for (int i = 0; i < 10; i++) {
+        robot_update(S, L, e);
+        space_step(S, L, e, dt);
+    }
+    int steps = S.episode_steps[e] + 1;
+    S.episode_steps[e] = steps;
+    bool d = max_steps > 0 && steps >= max_steps;
+    double sc = d ? score_env(S, L, e, cfg.task) : 0.0;
+    if (reward) reward[e] = (float)sc;
+    if (done) done[e] = d ? 1 : 0;
+    if (eval_score) eval_score[e] = sc;
+    if (d && auto_reset) reset_env(S, L, e, cfg); // VecEnv auto-reset: next obs is the new episode's first frame
+}
+
+__global__ void __launch_bounds__(64) bodies_kernel(MGState S, double *out, int32_t *counts) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= S.n_envs) return;
+    for (int b = 0; b < MG_MAX_BODIES; b++) {
+        double *o = out + ((size_t)e * MG_MAX_BODIES + b) * 6;
+        if (b < S.nbodies[e]) {
+            o[0] = AT(S.bpx, b); o[1] = AT(S.bpy, b); o[2] = AT(S.ba, b);
+            o[3] = AT(S.bvx, b); o[4] = AT(S.bvy, b); o[5] = AT(S.bw, b);
+        } else {
+            for (int k = 0; k < 6; k++) o[k] = 0.0;
+        }
+    }
+    if (counts) {
+        counts[4 * e + 0] = S.nbodies[e]; counts[4 * e + 1] = S.nshapes[e];
+        counts[4 * e + 2] = S.ncons[e]; counts[4 * e + 3] = S.nactive[e];
+    }
+}
+
+__global__ void __launch_bounds__(64) errors_kernel(MGState S, int32_t *out) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= S.n_envs) return;
+    out[e] = S.overflow[e];
+}
+
+// Philox4x32-10 (Salmon et al. 2011): counter = (step lo, step hi, env, 0), key = (k lo, k hi)
+__device__ __forceinline__ uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t &hi) {
+    uint64_t p = (uint64_t)a * b;
+    hi = (uint32_t)(p >> 32);
+    return (uint32_t)p;
+}
+__global__ void __launch_bounds__(256) actions_kernel(uint8_t *out, int n, uint64_t key, uint64_t step) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    uint32_t c0 = (uint32_t)step, c1 = (uint32_t)(step >> 32), c2 = (uint32_t)e, c3 = 0;
+    uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+    for (int r = 0; r < 10; r++) {
+        uint32_t hi0, hi1;
+        uint32_t lo0 = mulhilo(0xD2511F53u, c0, hi0);
+        uint32_t lo1 = mulhilo(0xCD9E8D57u, c2, hi1);
+        uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    out[e] = (uint8_t)(c0 % 18u);
+}
+
+// ---------------------------------------------------------------------------
+// allocation
+struct Carver {
+    char *base;
+    size_t off;
+    template <typename T> T *take(size_t n) {
+        off = (off + 255) & ~(size_t)255;
+        T *p = (T *)(base ? base + off : nullptr);
+        off += n * sizeof(T);
+        return p;
+    }
+};
+
+static void layout(MGState &S, Carver &c) {
+    size_t N = (size_t)S.N;
+    size_t B = MG_MAX_BODIES * N, SH = MG_MAX_SHAPES * N, C = MG_MAX_CONS * N, A = MG_MAX_ARB * N, E = MG_MAX_ENTS * N;
+    S.bpx = c.take<double>(B); S.bpy = c.take<double>(B); S.bvx = c.take<double>(B); S.bvy = c.take<double>(B);
+    S.ba = c.take<double>(B); S.bw = c.take<double>(B); S.bvbx = c.take<double>(B); S.bvby = c.take<double>(B);
+    S.bwb = c.take<double>(B); S.brc = c.take<double>(B); S.brs = c.take<double>(B); S.bminv = c.take<double>(B);
+    S.biinv = c.take<double>(B); S.bacache = c.take<double>(B); S.bkin = c.take<int8_t>(B);
+    S.nbodies = c.take<int32_t>(N);
+    S.sbody = c.take<int8_t>(SH); S.spoly = c.take<int8_t>(SH); S.sent = c.take<int8_t>(SH);
+    S.sgroup = c.take<int16_t>(SH); S.shash = c.take<int16_t>(SH); S.scat = c.take<uint8_t>(SH);
+    S.sr = c.take<double>(SH); S.su = c.take<double>(SH); S.sbbl = c.take<double>(SH); S.sbbb = c.take<double>(SH);
+    S.sbbr = c.take<double>(SH); S.sbbt = c.take<double>(SH);
+    S.nshapes = c.take<int32_t>(N);
+    S.ctype = c.take<int8_t>(C); S.ca = c.take<int8_t>(C); S.cb = c.take<int8_t>(C);
+    S.cp = c.take<double>((size_t)CP_NUM * C);
+    S.ncons = c.take<int32_t>(N);
+    S.akey = c.take<int32_t>(A); S.astamp = c.take<uint32_t>(A); S.astate = c.take<int8_t>(A);
+    S.acount = c.take<int8_t>(A); S.asa = c.take<int8_t>(A); S.asb = c.take<int8_t>(A);
+    S.anx = c.take<double>(A); S.any = c.take<double>(A); S.au = c.take<double>(A);
+    S.acon = c.take<double>((size_t)2 * AC_NUM * A); S.ahash = c.take<uint64_t>(2 * A);
+    S.active = c.take<int8_t>(A); S.nactive = c.take<int32_t>(N); S.stamp = c.take<uint32_t>(N);
+    S.curr_dt = c.take<double>(N); S.overflow = c.take<int32_t>(N);
+    S.target_speed = c.take<double>(N); S.rel_turn = c.take<double>(N); S.target_finger = c.take<double>(N);
+    S.robot_body0 = c.take<int32_t>(N); S.robot_cons0 = c.take<int32_t>(N); S.pv = c.take<double>(5 * N);
+    S.ekind = c.take<int8_t>(E); S.etype = c.take<int8_t>(E); S.ecol = c.take<int8_t>(E); S.erole = c.take<int8_t>(E);
+    S.ebody0 = c.take<int8_t>(E); S.eshape0 = c.take<int8_t>(E); S.enshapes = c.take<int8_t>(E);
+    S.ex = c.take<double>(E); S.ey = c.take<double>(E); S.eang = c.take<double>(E); S.eh = c.take<double>(E);
+    S.ew = c.take<double>(E); S.nents = c.take<int32_t>(N); S.gpx = c.take<double>(N); S.gpy = c.take<double>(N);
+    S.goal_ent = c.take<int32_t>(N); S.episode_steps = c.take<int32_t>(N);
+    S.mt_key = c.take<uint32_t>(624 * N); S.mt_pos = c.take<int32_t>(N);
+    size_t FR = (size_t)MG_LORES * MG_LORES * 3;
+    S.hist_allo = c.take<uint8_t>(4 * N * FR); S.hist_ego = c.take<uint8_t>(4 * N * FR);
+    S.hist_head = c.take<int32_t>(2 * N);
+}
+
+static hipStream_t as_stream(void *s) { return (hipStream_t)s; }
+static int grid64(const mg_sim *s) { return (s->S.n_envs + 63) / 64; }
+
+static int render_lores(mg_sim *s, hipStream_t st) {
+    RenderOut ro;
+    ro.full = nullptr;
+    ro.obs_allo = s->out.obs_allo; ro.obs_ego = s->out.obs_ego; ro.obs_past = s->out.obs_past;
+    ro.preproc = s->preproc;
+    hipLaunchKernelGGL(render_kernel, dim3(s->S.n_envs, 2), dim3(RG_THREADS), 0, st, s->S, s->dlib, ro, 0);
+    HIPC(hipGetLastError());
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+extern "C" {
+
+const char *mg_last_error(void) { return g_err.c_str(); }
+
+int mg_create(const mg_config *cfg, mg_sim **out) {
+    if (!cfg || !out) return set_err(-22, "mg_create: null argument");
+    if (cfg->library_size != (int64_t)sizeof(mg_library))
+        return set_err(-22, "mg_create: library_size mismatch (expected " + std::to_string(sizeof(mg_library)) + ")");
+    if (cfg->num_envs <= 0) return set_err(-22, "mg_create: num_envs must be positive");
+    if (cfg->task < 0 || cfg->task > 4) return set_err(-22, "mg_create: unknown task");
+    if (cfg->preproc != MG_PREPROC_LORES4E && cfg->preproc != MG_PREPROC_LORESSTACK &&
+        cfg->preproc != MG_PREPROC_LORES4A && cfg->preproc != MG_PREPROC_NONE)
+        return set_err(-95, "mg_create: preprocessor not supported by the GPU path");
+    HIPC(hipSetDevice(cfg->device));
+    mg_sim *s = new mg_sim();
+    memset(&s->S, 0, sizeof(MGState));
+    s->task = cfg->task; s->flags = cfg->rand_flags; s->preproc = cfg->preproc;
+    s->max_steps = cfg->max_episode_steps; s->device = cfg->device; s->auto_reset = cfg->auto_reset;
+    s->S.n_envs = cfg->num_envs;
+    s->S.N = (cfg->num_envs + 63) / 64 * 64;
+    Carver sizing = {nullptr, 0};
+    layout(s->S, sizing);
+    s->pool_bytes = sizing.off + 256;
+    hipError_t err = hipMalloc(&s->pool, s->pool_bytes);
+    if (err != hipSuccess) { delete s; return set_err(-12, std::string("mg_create: hipMalloc pool: ") + hipGetErrorString(err)); }
+    HIPC(hipMemset(s->pool, 0, s->pool_bytes));
+    Carver real = {(char *)s->pool, 0};
+    layout(s->S, real);
+    err = hipMalloc((void **)&s->dlib, sizeof(mg_library));
+    if (err != hipSuccess) { hipFree(s->pool); delete s; return set_err(-12, "mg_create: hipMalloc library"); }
+    HIPC(hipMemcpy(s->dlib, cfg->library, sizeof(mg_library), hipMemcpyHostToDevice));
+    std::vector<uint32_t> seeds(cfg->num_envs);
+    for (int i = 0; i < cfg->num_envs; i++) seeds[i] = cfg->seeds ? cfg->seeds[i] : cfg->base_seed + (uint32_t)i;
+    *out = s;
+    return mg_seed(s, seeds.data());
+}
+
+int mg_seed(mg_sim *s, const uint32_t *seeds_host) {
+    if (!s || !seeds_host) return set_err(-22, "mg_seed: null argument");
+    HIPC(hipSetDevice(s->device));
+    uint32_t *d = nullptr;
+    HIPC(hipMalloc(&d, sizeof(uint32_t) * s->S.n_envs));
+    HIPC(hipMemcpy(d, seeds_host, sizeof(uint32_t) * s->S.n_envs, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(seed_kernel, dim3(grid64(s)), dim3(64), 0, 0, s->S, d);
+    HIPC(hipGetLastError());
+    HIPC(hipDeviceSynchronize());
+    HIPC(hipFree(d));
+    return 0;
+}
+
+int mg_bind_outputs(mg_sim *s, const mg_buffers *b) {
+    if (!s || !b) return set_err(-22, "mg_bind_outputs: null argument");
+    if (s->preproc != MG_PREPROC_NONE && (!b->obs_allo || !b->obs_ego))
+        return set_err(-22, "mg_bind_outputs: obs_allo / obs_ego required");
+    if ((s->preproc == MG_PREPROC_LORES4E || s->preproc == MG_PREPROC_LORES4A) && !b->obs_past)
+        return set_err(-22, "mg_bind_outputs: obs_past required for this preprocessor");
+    s->out = *b;
+    s->bound = 1;
+    return 0;
+}
+
+int mg_reset(mg_sim *s, const uint8_t *mask, void *stream) {
+    if (!s) return set_err(-22, "mg_reset: null sim");
+    if (!s->bound && s->preproc != MG_PREPROC_NONE) return set_err(-22, "mg_reset: outputs not bound");
+    HIPC(hipSetDevice(s->device));
+    hipStream_t st = as_stream(stream);
+    TaskCfg cfg = {s->task, s->flags};
+    hipLaunchKernelGGL(reset_kernel, dim3(grid64(s)), dim3(64), 0, st, s->S, s->dlib, cfg, mask);
+    HIPC(hipGetLastError());
+    if (s->preproc != MG_PREPROC_NONE) return render_lores(s, st);
+    return 0;
+}
+
+int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
+    if (!s || !actions) return set_err(-22, "mg_step: null argument");
+    if (!s->bound && s->preproc != MG_PREPROC_NONE) return set_err(-22, "mg_step: outputs not bound");
+    HIPC(hipSetDevice(s->device));
+    hipStream_t st = as_stream(stream);
+    TaskCfg cfg = {s->task, s->flags};
+    hipLaunchKernelGGL(step_kernel, dim3(grid64(s)), dim3(64), 0, st, s->S, s->dlib, cfg, s->max_steps, s->auto_reset, actions,
+                       s->out.reward, s->out.done, s->out.eval_score);
+    HIPC(hipGetLastError());
+    if (s->preproc != MG_PREPROC_NONE) return render_lores(s, st);
+    return 0;
+}
+
+int mg_render_full(mg_sim *s, uint8_t *out, void *stream) {
+    if (!s || !out) return set_err(-22, "mg_render_full: null argument");
+    HIPC(hipSetDevice(s->device));
+    RenderOut ro;
+    memset(&ro, 0, sizeof(ro));
+    ro.full = out;
+    ro.preproc = s->preproc;
+    hipLaunchKernelGGL(render_kernel, dim3(s->S.n_envs, 2), dim3(RG_THREADS), 0, as_stream(stream), s->S, s->dlib, ro, 1);
+    HIPC(hipGetLastError());
+    return 0;
+}
+
+int mg_get_bodies(mg_sim *s, double *out, int32_t *counts, void *stream) {
+    if (!s || !out) return set_err(-22, "mg_get_bodies: null argument");
+    HIPC(hipSetDevice(s->device));
+    hipLaunchKernelGGL(bodies_kernel, dim3(grid64(s)), dim3(64), 0, as_stream(stream), s->S, out, counts);
+    HIPC(hipGetLastError());
+    return 0;
+}
+
+int mg_get_errors(mg_sim *s, int32_t *out, void *stream) {
+    if (!s || !out) return set_err(-22, "mg_get_errors: null argument");
+    HIPC(hipSetDevice(s->device));
+    hipLaunchKernelGGL(errors_kernel, dim3(grid64(s)), dim3(64), 0, as_stream(stream), s->S, out);
+    HIPC(hipGetLastError());
+    return 0;
+}
+
+int mg_random_actions(mg_sim *s, uint8_t *actions, uint64_t key, uint64_t step, void *stream) {
+    if (!s || !actions) return set_err(-22, "mg_random_actions: null argument");
+    HIPC(hipSetDevice(s->device));
+    hipLaunchKernelGGL(actions_kernel, dim3((s->S.n_envs + 255) / 256), dim3(256), 0, as_stream(stream), actions,
+                       s->S.n_envs, key, step);
+    HIPC(hipGetLastError());
+    return 0;
+}
+
+int mg_num_envs(const mg_sim *s) { return s ? s->S.n_envs : -22; }
+
+void mg_destroy(mg_sim *s) {
+    if (!s) return;
+    hipSetDevice(s->device);
+    hipFree(s->pool);
+    hipFree(s->dlib);
+    delete s;
+}
+
+} // extern "C"

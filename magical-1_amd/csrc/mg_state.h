@@ -1,0 +1,77 @@
+// mg_state.h -- per-env structure-of-arrays state of the batched simulator.
+//
+// Every array is [slot][N] with N the env count padded to a multiple of 64:
+// lane l of a wavefront owns env (64*wave + l), so each field access of a
+// wavefront is one contiguous 512-byte (double) / 64-byte (int8) segment.
+// Physics runs one env per lane (Chipmunk's sequential-impulse solver is a
+// Gauss-Seidel sweep in a fixed order, so the parallelism is across envs);
+// rendering runs one workgroup per (env, view).
+#pragma once
+#include "mg_common.h"
+
+struct MGState {
+    int N;      // padded env count (multiple of 64)
+    int n_envs; // live env count
+    // ---- bodies [MG_MAX_BODIES][N] ----
+    double *bpx, *bpy, *bvx, *bvy, *ba, *bw, *bvbx, *bvby, *bwb, *brc, *brs, *bminv, *biinv, *bacache;
+    int8_t *bkin;   // 1 = kinematic
+    int32_t *nbodies;
+    // ---- dynamic shapes [MG_MAX_SHAPES][N] ----
+    int8_t *sbody, *spoly, *sent; // body slot; library poly id (-1 circle); owning entity
+    int16_t *sgroup, *shash; // filter group; Chipmunk shape hashid (global add index)
+    uint8_t *scat;  // categories != 0 (pm_randomise_all_poses disables shapes)
+    double *sr, *su, *sbbl, *sbbb, *sbbr, *sbbt;
+    int32_t *nshapes;
+    // ---- constraints [MG_MAX_CONS][N] ----
+    int8_t *ctype, *ca, *cb; // -1 = static body
+    double *cp;              // [16][MG_MAX_CONS][N] parameters / accumulators, see mg_phys.h
+    int32_t *ncons;
+    // ---- arbiters [MG_MAX_ARB][N] ----
+    int32_t *akey;           // lo * 128 + hi, -1 = free
+    uint32_t *astamp;
+    int8_t *astate, *acount, *asa, *asb; // asa/asb: body slots of shapes a, b (-1 static)
+    double *anx, *any, *au;
+    double *acon;            // [2 contacts][10 fields][MG_MAX_ARB][N]
+    uint64_t *ahash;         // [2][MG_MAX_ARB][N]
+    int8_t *active;          // [MG_MAX_ARB][N]
+    int32_t *nactive;
+    uint32_t *stamp;
+    double *curr_dt;
+    int32_t *overflow;       // per env error flags
+    // ---- robot control + physics variables [N] ----
+    double *target_speed, *rel_turn, *target_finger;
+    int32_t *robot_body0, *robot_cons0;
+    double *pv;              // [5][N]
+    // ---- entities [MG_MAX_ENTS][N] ----
+    int8_t *ekind, *etype, *ecol, *erole, *ebody0, *eshape0, *enshapes;
+    double *ex, *ey, *eang, *eh, *ew;
+    int32_t *nents;
+    double *gpx, *gpy;       // goal body position [N] (static sensor)
+    int32_t *goal_ent;       // [N] (-1 none)
+    // ---- episode ----
+    int32_t *episode_steps;
+    // ---- RNG: numpy legacy MT19937 per env ----
+    uint32_t *mt_key;        // [624][N]
+    int32_t *mt_pos;         // [N]
+    // ---- LoRes frame history (downsampled, newest last) ----
+    uint8_t *hist_allo;      // [4][N][96*96*3]
+    uint8_t *hist_ego;       // [4][N][96*96*3]
+    int32_t *hist_head;      // [N] ring head
+};
+
+// constraint parameter slots (cp[k][c][env])
+enum {
+    CP_MAXF = 0, CP_MAXB = 1, CP_BCOEF = 2, CP_JACC = 3, CP_JACC2 = 4, CP_ISUM = 5, CP_BIAS = 6, CP_BIAS2 = 7,
+    // pivot
+    CP_AAX = 8, CP_AAY = 9, CP_ABX = 10, CP_ABY = 11, CP_R1X = 12, CP_R1Y = 13, CP_R2X = 14, CP_R2Y = 15,
+    CP_K11 = 16, CP_K12 = 17, CP_K21 = 18, CP_K22 = 19,
+    // gear / limit / motor / spring reuse 8..
+    CP_PHASE = 8, CP_RATIO = 9, CP_RATIO_INV = 10,
+    CP_MIN = 8, CP_MAX = 9,
+    CP_RATE = 8,
+    CP_REST = 8, CP_STIFF = 9, CP_WCOEF = 10, CP_TWRN = 11,
+    CP_NUM = 20
+};
+// contact fields (acon[k][field][arb][env])
+enum { AC_R1X = 0, AC_R1Y, AC_R2X, AC_R2Y, AC_NMASS, AC_TMASS, AC_JN, AC_JT, AC_JB, AC_BIAS, AC_NUM };
+enum { ARB_FIRST = 0, ARB_NORMAL = 1, ARB_CACHED = 3 };

@@ -1,0 +1,408 @@
+// mg_step.h -- one env-step of physics per lane: Robot.update + cpSpaceStep x10.
+//
+// base_env.py:267-276 (action -> Robot.set_action), entities.py:435-476
+// (Robot.set_action / Robot.update), base_env.py:248-255 (10 substeps).
+#pragma once
+#include "mg_phys.h"
+
+// ---- body access with the static body as zeros --------------------------
+struct BodyR { int b; double minv, iinv; };
+MG_DEV BodyR bodyr(const MGState &S, int e, int b) {
+    if (b < 0) return {b, 0.0, 0.0};
+    return {b, AT(S.bminv, b), AT(S.biinv, b)};
+}
+MG_DEV V2 bv(const MGState &S, int e, int b) { return b < 0 ? v2(0.0, 0.0) : v2(AT(S.bvx, b), AT(S.bvy, b)); }
+MG_DEV double bwv(const MGState &S, int e, int b) { return b < 0 ? 0.0 : AT(S.bw, b); }
+MG_DEV V2 bvb(const MGState &S, int e, int b) { return b < 0 ? v2(0.0, 0.0) : v2(AT(S.bvbx, b), AT(S.bvby, b)); }
+MG_DEV double bwb(const MGState &S, int e, int b) { return b < 0 ? 0.0 : AT(S.bwb, b); }
+MG_DEV V2 bp(const MGState &S, int e, int b) { return b < 0 ? v2(0.0, 0.0) : v2(AT(S.bpx, b), AT(S.bpy, b)); }
+MG_DEV double ban(const MGState &S, int e, int b) { return b < 0 ? 0.0 : AT(S.ba, b); }
+
+MG_DEV void apply_impulse(const MGState &S, int e, const BodyR &B, V2 j, V2 r) {
+    if (B.b < 0) return;
+    AT(S.bvx, B.b) = AT(S.bvx, B.b) + j.x * B.minv;
+    AT(S.bvy, B.b) = AT(S.bvy, B.b) + j.y * B.minv;
+    AT(S.bw, B.b) += B.iinv * vcross(r, j);
+}
+MG_DEV void apply_impulses(const MGState &S, int e, const BodyR &A, const BodyR &B, V2 r1, V2 r2, V2 j) {
+    apply_impulse(S, e, A, vneg(j), r1);
+    apply_impulse(S, e, B, j, r2);
+}
+MG_DEV void apply_bias_impulse(const MGState &S, int e, const BodyR &B, V2 j, V2 r) {
+    if (B.b < 0) return;
+    AT(S.bvbx, B.b) = AT(S.bvbx, B.b) + j.x * B.minv;
+    AT(S.bvby, B.b) = AT(S.bvby, B.b) + j.y * B.minv;
+    AT(S.bwb, B.b) += B.iinv * vcross(r, j);
+}
+MG_DEV V2 relative_velocity(const MGState &S, int e, int a, int b, V2 r1, V2 r2) {
+    V2 v1 = vadd(bv(S, e, a), vmult(vperp(r1), bwv(S, e, a)));
+    V2 v2_ = vadd(bv(S, e, b), vmult(vperp(r2), bwv(S, e, b)));
+    return vsub(v2_, v1);
+}
+MG_DEV double k_scalar_body(const BodyR &B, V2 r, V2 n) {
+    double rcn = vcross(r, n);
+    return B.minv + B.iinv * rcn * rcn;
+}
+
+// ---- constraints ----------------------------------------------------------
+MG_DEV void cons_prestep(const MGState &S, int e, int c, double dt) {
+    int a = AT(S.ca, c), b = AT(S.cb, c);
+    BodyR A = bodyr(S, e, a), B = bodyr(S, e, b);
+    switch (AT(S.ctype, c)) {
+    case MG_C_PIVOT: {
+        double ac = a < 0 ? 1.0 : AT(S.brc, a), as = a < 0 ? 0.0 : AT(S.brs, a);
+        double bc = AT(S.brc, b), bs = AT(S.brs, b);
+        V2 aa = vsub(v2(CPA(CP_AAX, c), CPA(CP_AAY, c)), v2(0.0, 0.0));
+        V2 ab = vsub(v2(CPA(CP_ABX, c), CPA(CP_ABY, c)), v2(0.0, 0.0));
+        V2 r1 = v2(ac * aa.x + (-as) * aa.y, as * aa.x + ac * aa.y);
+        V2 r2 = v2(bc * ab.x + (-bs) * ab.y, bs * ab.x + bc * ab.y);
+        CPA(CP_R1X, c) = r1.x; CPA(CP_R1Y, c) = r1.y; CPA(CP_R2X, c) = r2.x; CPA(CP_R2Y, c) = r2.y;
+        double m_sum = A.minv + B.minv;
+        double k11 = m_sum, k12 = 0.0, k21 = 0.0, k22 = m_sum;
+        double r1xsq = r1.x * r1.x * A.iinv, r1ysq = r1.y * r1.y * A.iinv, r1nxy = -r1.x * r1.y * A.iinv;
+        k11 += r1ysq; k12 += r1nxy; k21 += r1nxy; k22 += r1xsq;
+        double r2xsq = r2.x * r2.x * B.iinv, r2ysq = r2.y * r2.y * B.iinv, r2nxy = -r2.x * r2.y * B.iinv;
+        k11 += r2ysq; k12 += r2nxy; k21 += r2nxy; k22 += r2xsq;
+        double det = k11 * k22 - k12 * k21;
+        double det_inv = 1.0 / det;
+        CPA(CP_K11, c) = k22 * det_inv; CPA(CP_K12, c) = -k12 * det_inv;
+        CPA(CP_K21, c) = -k21 * det_inv; CPA(CP_K22, c) = k11 * det_inv;
+        V2 delta = vsub(vadd(bp(S, e, b), r2), vadd(bp(S, e, a), r1));
+        V2 bias = vclamp(vmult(delta, -CPA(CP_BCOEF, c) / dt), CPA(CP_MAXB, c));
+        CPA(CP_BIAS, c) = bias.x; CPA(CP_BIAS2, c) = bias.y;
+        break;
+    }
+    case MG_C_GEAR: {
+        CPA(CP_ISUM, c) = 1.0 / (A.iinv * CPA(CP_RATIO_INV, c) + CPA(CP_RATIO, c) * B.iinv);
+        double maxBias = CPA(CP_MAXB, c);
+        CPA(CP_BIAS, c) = cpclamp(-CPA(CP_BCOEF, c) * (ban(S, e, b) * CPA(CP_RATIO, c) - ban(S, e, a) - CPA(CP_PHASE, c)) / dt,
+                                  -maxBias, maxBias);
+        break;
+    }
+    case MG_C_ROTLIMIT: {
+        double dist = ban(S, e, b) - ban(S, e, a), pdist = 0.0;
+        double mx = CPA(CP_MAX, c), mn = CPA(CP_MIN, c);
+        if (dist > mx) pdist = mx - dist;
+        else if (dist < mn) pdist = mn - dist;
+        CPA(CP_ISUM, c) = 1.0 / (A.iinv + B.iinv);
+        double maxBias = CPA(CP_MAXB, c);
+        double bias = cpclamp(-CPA(CP_BCOEF, c) * pdist / dt, -maxBias, maxBias);
+        CPA(CP_BIAS, c) = bias;
+        if (!bias) CPA(CP_JACC, c) = 0.0;
+        break;
+    }
+    case MG_C_MOTOR:
+        CPA(CP_ISUM, c) = 1.0 / (A.iinv + B.iinv);
+        break;
+    case MG_C_SPRING: {
+        double moment = A.iinv + B.iinv;
+        CPA(CP_ISUM, c) = 1.0 / moment;
+        CPA(CP_TWRN, c) = 0.0;
+        double j_spring = ((ban(S, e, a) - ban(S, e, b)) - CPA(CP_REST, c)) * CPA(CP_STIFF, c) * dt;
+        CPA(CP_JACC, c) = j_spring;
+        if (a >= 0) AT(S.bw, a) -= j_spring * A.iinv;
+        if (b >= 0) AT(S.bw, b) += j_spring * B.iinv;
+        break;
+    }
+    }
+}
+
+MG_DEV void cons_cached(const MGState &S, int e, int c, double dt_coef) {
+    int a = AT(S.ca, c), b = AT(S.cb, c);
+    BodyR A = bodyr(S, e, a), B = bodyr(S, e, b);
+    switch (AT(S.ctype, c)) {
+    case MG_C_PIVOT:
+        apply_impulses(S, e, A, B, v2(CPA(CP_R1X, c), CPA(CP_R1Y, c)), v2(CPA(CP_R2X, c), CPA(CP_R2Y, c)),
+                       vmult(v2(CPA(CP_JACC, c), CPA(CP_JACC2, c)), dt_coef));
+        break;
+    case MG_C_GEAR: {
+        double j = CPA(CP_JACC, c) * dt_coef;
+        if (a >= 0) AT(S.bw, a) -= j * A.iinv * CPA(CP_RATIO_INV, c);
+        if (b >= 0) AT(S.bw, b) += j * B.iinv;
+        break;
+    }
+    case MG_C_ROTLIMIT:
+    case MG_C_MOTOR: {
+        double j = CPA(CP_JACC, c) * dt_coef;
+        if (a >= 0) AT(S.bw, a) -= j * A.iinv;
+        if (b >= 0) AT(S.bw, b) += j * B.iinv;
+        break;
+    }
+    default: break;
+    }
+}
+
+MG_DEV void cons_apply(const MGState &S, int e, int c, double dt) {
+    int a = AT(S.ca, c), b = AT(S.cb, c);
+    BodyR A = bodyr(S, e, a), B = bodyr(S, e, b);
+    switch (AT(S.ctype, c)) {
+    case MG_C_PIVOT: {
+        V2 r1 = v2(CPA(CP_R1X, c), CPA(CP_R1Y, c)), r2 = v2(CPA(CP_R2X, c), CPA(CP_R2Y, c));
+        V2 vr = relative_velocity(S, e, a, b, r1, r2);
+        V2 d = vsub(v2(CPA(CP_BIAS, c), CPA(CP_BIAS2, c)), vr);
+        V2 j = v2(d.x * CPA(CP_K11, c) + d.y * CPA(CP_K12, c), d.x * CPA(CP_K21, c) + d.y * CPA(CP_K22, c));
+        V2 jOld = v2(CPA(CP_JACC, c), CPA(CP_JACC2, c));
+        V2 jAcc = vclamp(vadd(jOld, j), CPA(CP_MAXF, c) * dt);
+        CPA(CP_JACC, c) = jAcc.x; CPA(CP_JACC2, c) = jAcc.y;
+        apply_impulses(S, e, A, B, r1, r2, vsub(jAcc, jOld));
+        break;
+    }
+    case MG_C_GEAR: {
+        double ratio = CPA(CP_RATIO, c);
+        double wr = bwv(S, e, b) * ratio - bwv(S, e, a);
+        double jMax = CPA(CP_MAXF, c) * dt;
+        double j = (CPA(CP_BIAS, c) - wr) * CPA(CP_ISUM, c);
+        double jOld = CPA(CP_JACC, c);
+        double jAcc = cpclamp(jOld + j, -jMax, jMax);
+        CPA(CP_JACC, c) = jAcc;
+        j = jAcc - jOld;
+        if (a >= 0) AT(S.bw, a) -= j * A.iinv * CPA(CP_RATIO_INV, c);
+        if (b >= 0) AT(S.bw, b) += j * B.iinv;
+        break;
+    }
+    case MG_C_ROTLIMIT: {
+        double bias = CPA(CP_BIAS, c);
+        if (!bias) return;
+        double wr = bwv(S, e, b) - bwv(S, e, a);
+        double jMax = CPA(CP_MAXF, c) * dt;
+        double j = -(bias + wr) * CPA(CP_ISUM, c);
+        double jOld = CPA(CP_JACC, c);
+        double jAcc = bias < 0.0 ? cpclamp(jOld + j, 0.0, jMax) : cpclamp(jOld + j, -jMax, 0.0);
+        CPA(CP_JACC, c) = jAcc;
+        j = jAcc - jOld;
+        if (a >= 0) AT(S.bw, a) -= j * A.iinv;
+        if (b >= 0) AT(S.bw, b) += j * B.iinv;
+        break;
+    }
+    case MG_C_MOTOR: {
+        double wr = bwv(S, e, b) - bwv(S, e, a) + CPA(CP_RATE, c);
+        double jMax = CPA(CP_MAXF, c) * dt;
+        double j = -wr * CPA(CP_ISUM, c);
+        double jOld = CPA(CP_JACC, c);
+        double jAcc = cpclamp(jOld + j, -jMax, jMax);
+        CPA(CP_JACC, c) = jAcc;
+        j = jAcc - jOld;
+        if (a >= 0) AT(S.bw, a) -= j * A.iinv;
+        if (b >= 0) AT(S.bw, b) += j * B.iinv;
+        break;
+    }
+    case MG_C_SPRING: {
+        double wrn = bwv(S, e, a) - bwv(S, e, b);
+        double w_damp = (CPA(CP_TWRN, c) - wrn) * CPA(CP_WCOEF, c);
+        CPA(CP_TWRN, c) = wrn + w_damp;
+        double j_damp = w_damp * CPA(CP_ISUM, c);
+        CPA(CP_JACC, c) += j_damp;
+        if (a >= 0) AT(S.bw, a) += j_damp * A.iinv;
+        if (b >= 0) AT(S.bw, b) -= j_damp * B.iinv;
+        break;
+    }
+    }
+}
+
+// ---- arbiters ------------------------------------------------------------
+MG_DEV void arbiter_update(const MGState &S, const mg_library *L, int e, int key, const ShapeW &A, const ShapeW &B,
+                           double ua, double ub, const Collision &info) {
+    int na = MG_MAX_ARB, slot = -1, free_slot = -1;
+    for (int i = 0; i < na; i++) {
+        int k = AT(S.akey, i);
+        if (k == key) { slot = i; break; }
+        if (k < 0 && free_slot < 0) free_slot = i;
+    }
+    if (slot < 0) {
+        if (free_slot < 0) { S.overflow[e] |= 1; return; }
+        slot = free_slot;
+        AT(S.akey, slot) = key; AT(S.astate, slot) = ARB_FIRST; AT(S.acount, slot) = 0; AT(S.astamp, slot) = 0;
+    }
+    // info is in collision order: swapped => (a, b) = (B, A)
+    const ShapeW &sa = info.count >= 0 && A.type > B.type ? B : A;
+    const ShapeW &sb = A.type > B.type ? A : B;
+    double u_a = A.type > B.type ? ub : ua, u_b = A.type > B.type ? ua : ub;
+    V2 pa = bp(S, e, sa.body), pb = bp(S, e, sb.body);
+    int oldc = AT(S.acount, slot);
+    uint64_t oh0 = AHASH(0, slot), oh1 = AHASH(1, slot);
+    double ojn0 = ACON(0, AC_JN, slot), ojt0 = ACON(0, AC_JT, slot);
+    double ojn1 = ACON(1, AC_JN, slot), ojt1 = ACON(1, AC_JT, slot);
+    for (int k = 0; k < info.count; k++) {
+        V2 r1 = vsub(info.p1[k], pa), r2 = vsub(info.p2[k], pb);
+        double jn = 0.0, jt = 0.0;
+        uint64_t h = info.hash[k];
+        if (oldc > 0 && h == oh0) { jn = ojn0; jt = ojt0; }
+        if (oldc > 1 && h == oh1) { jn = ojn1; jt = ojt1; }
+        ACON(k, AC_R1X, slot) = r1.x; ACON(k, AC_R1Y, slot) = r1.y;
+        ACON(k, AC_R2X, slot) = r2.x; ACON(k, AC_R2Y, slot) = r2.y;
+        ACON(k, AC_JN, slot) = jn; ACON(k, AC_JT, slot) = jt;
+        AHASH(k, slot) = h;
+    }
+    AT(S.acount, slot) = info.count;
+    AT(S.anx, slot) = info.n.x; AT(S.any, slot) = info.n.y;
+    AT(S.au, slot) = u_a * u_b;
+    AT(S.asa, slot) = sa.body; AT(S.asb, slot) = sb.body;
+    if (AT(S.astate, slot) == ARB_CACHED) AT(S.astate, slot) = ARB_FIRST;
+    int na_ = S.nactive[e];
+    if (na_ < MG_MAX_ARB) { AT(S.active, na_) = slot; S.nactive[e] = na_ + 1; }
+    else S.overflow[e] |= 1;
+    AT(S.astamp, slot) = S.stamp[e];
+}
+
+MG_DEV void arbiter_prestep(const MGState &S, const mg_library *L, int e, int slot, double dt) {
+    int a = AT(S.asa, slot), b = AT(S.asb, slot);
+    BodyR A = bodyr(S, e, a), B = bodyr(S, e, b);
+    V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
+    V2 body_delta = vsub(bp(S, e, b), bp(S, e, a));
+    int cnt = AT(S.acount, slot);
+    for (int k = 0; k < cnt; k++) {
+        V2 r1 = v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)), r2 = v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot));
+        ACON(k, AC_NMASS, slot) = 1.0 / (k_scalar_body(A, r1, n) + k_scalar_body(B, r2, n));
+        V2 pn = vperp(n);
+        ACON(k, AC_TMASS, slot) = 1.0 / (k_scalar_body(A, r1, pn) + k_scalar_body(B, r2, pn));
+        double dist = vdot(vadd(vsub(r2, r1), body_delta), n);
+        ACON(k, AC_BIAS, slot) = -L->collision_bias_coef * cpmin(0.0, dist + L->slop) / dt;
+        ACON(k, AC_JB, slot) = 0.0;
+    }
+}
+
+MG_DEV void arbiter_cached(const MGState &S, int e, int slot, double dt_coef) {
+    if (AT(S.astate, slot) == ARB_FIRST) return;
+    int a = AT(S.asa, slot), b = AT(S.asb, slot);
+    BodyR A = bodyr(S, e, a), B = bodyr(S, e, b);
+    V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
+    int cnt = AT(S.acount, slot);
+    for (int k = 0; k < cnt; k++) {
+        V2 j = vrotate(n, v2(ACON(k, AC_JN, slot), ACON(k, AC_JT, slot)));
+        apply_impulses(S, e, A, B, v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)),
+                       v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot)), vmult(j, dt_coef));
+    }
+}
+
+MG_DEV void arbiter_apply(const MGState &S, int e, int slot) {
+    int a = AT(S.asa, slot), b = AT(S.asb, slot);
+    BodyR A = bodyr(S, e, a), B = bodyr(S, e, b);
+    V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
+    double friction = AT(S.au, slot);
+    int cnt = AT(S.acount, slot);
+    for (int k = 0; k < cnt; k++) {
+        double nMass = ACON(k, AC_NMASS, slot);
+        V2 r1 = v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)), r2 = v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot));
+        V2 vb1 = vadd(bvb(S, e, a), vmult(vperp(r1), bwb(S, e, a)));
+        V2 vb2 = vadd(bvb(S, e, b), vmult(vperp(r2), bwb(S, e, b)));
+        V2 vr = relative_velocity(S, e, a, b, r1, r2);
+        double vbn = vdot(vsub(vb2, vb1), n);
+        double vrn = vdot(vr, n);
+        double vrt = vdot(vr, vperp(n));
+        double jbn = (ACON(k, AC_BIAS, slot) - vbn) * nMass;
+        double jbnOld = ACON(k, AC_JB, slot);
+        double jBias = cpmax(jbnOld + jbn, 0.0);
+        ACON(k, AC_JB, slot) = jBias;
+        double jn = -(0.0 + vrn) * nMass;
+        double jnOld = ACON(k, AC_JN, slot);
+        double jnAcc = cpmax(jnOld + jn, 0.0);
+        ACON(k, AC_JN, slot) = jnAcc;
+        double jtMax = friction * jnAcc;
+        double jt = -vrt * ACON(k, AC_TMASS, slot);
+        double jtOld = ACON(k, AC_JT, slot);
+        double jtAcc = cpclamp(jtOld + jt, -jtMax, jtMax);
+        ACON(k, AC_JT, slot) = jtAcc;
+        V2 jb = vmult(n, jBias - jbnOld);
+        apply_bias_impulse(S, e, A, vneg(jb), r1);
+        apply_bias_impulse(S, e, B, jb, r2);
+        apply_impulses(S, e, A, B, r1, r2, vrotate(n, v2(jnAcc - jnOld, jtAcc - jtOld)));
+    }
+}
+
+// ---- cpSpaceStep -----------------------------------------------------------
+MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt) {
+    uint32_t stamp = S.stamp[e] + 1;
+    S.stamp[e] = stamp;
+    double prev_dt = S.curr_dt[e];
+    S.curr_dt[e] = dt;
+    int nact = S.nactive[e];
+    for (int i = 0; i < nact; i++) AT(S.astate, AT(S.active, i)) = ARB_NORMAL;
+    S.nactive[e] = 0;
+    int nb = S.nbodies[e];
+    for (int b = 0; b < nb; b++) {
+        AT(S.bpx, b) = AT(S.bpx, b) + (AT(S.bvx, b) + AT(S.bvbx, b)) * dt;
+        AT(S.bpy, b) = AT(S.bpy, b) + (AT(S.bvy, b) + AT(S.bvby, b)) * dt;
+        body_set_angle(S, e, b, AT(S.ba, b) + (AT(S.bw, b) + AT(S.bwb, b)) * dt);
+        AT(S.bvbx, b) = 0.0; AT(S.bvby, b) = 0.0; AT(S.bwb, b) = 0.0;
+    }
+    int ns = S.nshapes[e];
+    for (int k = 0; k < ns; k++) shape_update_bb(S, L, e, k);
+    // broadphase + narrowphase, canonical order
+    for (int i = 0; i < ns; i++) {
+        ShapeW A;
+        load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A);
+        int gi = AT(S.sgroup, i), bi = AT(S.sbody, i);
+        double ui = AT(S.su, i);
+        for (int w = 0; w < 4; w++) {
+            ShapeW W;
+            load_wall(w, W);
+            if (!bb_intersects(A, W)) continue;
+            Collision info;
+            collide(A, W, info);
+            if (info.count) arbiter_update(S, L, e, i * 128 + 100 + w, A, W, ui, 0.8, info);
+        }
+        for (int j = i + 1; j < ns; j++) {
+            if (!(A.bbl <= AT(S.sbbr, j) && AT(S.sbbl, j) <= A.bbr && A.bbb <= AT(S.sbbt, j) && AT(S.sbbb, j) <= A.bbt))
+                continue;
+            if (AT(S.sbody, j) == bi) continue;
+            int gj = AT(S.sgroup, j);
+            if (gi != 0 && gi == gj) continue;
+            ShapeW B;
+            load_shape(S, L, e, j, (uint64_t)AT(S.shash, j), B);
+            Collision info;
+            collide(A, B, info);
+            if (info.count) arbiter_update(S, L, e, i * 128 + j, A, B, ui, AT(S.su, j), info);
+        }
+    }
+    // cached arbiter filter
+    for (int i = 0; i < MG_MAX_ARB; i++) {
+        if (AT(S.akey, i) < 0) continue;
+        uint32_t ticks = stamp - AT(S.astamp, i);
+        if (ticks >= 1 && AT(S.astate, i) != ARB_CACHED) AT(S.astate, i) = ARB_CACHED;
+        if (ticks >= 3) { AT(S.akey, i) = -1; AT(S.acount, i) = 0; }
+    }
+    nact = S.nactive[e];
+    int nc = S.ncons[e];
+    for (int i = 0; i < nact; i++) arbiter_prestep(S, L, e, AT(S.active, i), dt);
+    for (int c = 0; c < nc; c++) cons_prestep(S, e, c, dt);
+    // velocity integration is the identity here (no gravity, damping 1, no forces)
+    double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
+    for (int i = 0; i < nact; i++) arbiter_cached(S, e, AT(S.active, i), dt_coef);
+    for (int c = 0; c < nc; c++) cons_cached(S, e, c, dt_coef);
+    for (int it = 0; it < 10; it++) {
+        for (int i = 0; i < nact; i++) arbiter_apply(S, e, AT(S.active, i));
+        for (int c = 0; c < nc; c++) cons_apply(S, e, c, dt);
+    }
+}
+
+// ---- robot control ---------------------------------------------------------
+MG_DEV void robot_set_action(const MGState &S, const mg_library *L, int e, int action) {
+    const int ud = action % 3, lr = (action / 3) % 3;
+    double radius = L->robot_radius;
+    double ts = 0.0, turn = 0.0;
+    if (ud == 1) ts += 4.0 * radius;
+    if (ud == 2) ts -= 3.0 * radius;
+    if (lr == 1) turn += 1.5;
+    if (lr == 2) turn -= 1.5;
+    S.target_speed[e] = ts;
+    S.rel_turn[e] = turn;
+    S.target_finger[e] = action < 9 ? L->finger_angle_off[0] : -0.0; // OPEN: pi/8, CLOSE: -finger_rot_limit_inner
+}
+
+MG_DEV void robot_update(const MGState &S, const mg_library *L, int e) {
+    int body = S.robot_body0[e], control = body + 1, cons0 = S.robot_cons0[e];
+    body_set_angle(S, e, control, AT(S.ba, body) + S.rel_turn[e]);
+    double c = AT(S.brc, body), s = AT(S.brs, body), ts = S.target_speed[e];
+    AT(S.bvx, control) = c * 0.0 - s * ts;
+    AT(S.bvy, control) = c * ts + s * 0.0;
+    double tf = S.target_finger[e];
+    for (int k = 0; k < 2; k++) {
+        double side = k == 0 ? -1.0 : 1.0;
+        double rel = AT(S.ba, body + 4 + k) - AT(S.ba, body);
+        double x = (rel + side * tf) * 10;
+        double tr = (x < 1) ? x : 1.0;
+        tr = (tr > -1) ? tr : -1.0;
+        if (fabs(tr) < 1e-4) tr = 0.0;
+        CPA(CP_RATE, cons0 + 6 + 3 * k) = tr;
+    }
+}

@@ -1,0 +1,243 @@
+"""Gym-style surfaces over the GPU simulator.
+
+* VecMagicalEnv -- N instances of one registered name on one GPU (batched
+  counterpart of gym.make(name) under SB3's DummyVecEnv, train_rl.py:87-92):
+  reset() -> dict of uint8 device tensors, step(actions) -> (obs, reward f32,
+  done bool, {'eval_score': f64}); finished episodes auto-reset in place.
+* MagicalEnv -- one instance with the single-env gym API of
+  BaseEnv + preprocessors (base_env.py:190-351, benchmarks/__init__.py:51-190):
+  numpy observations, done at max_episode_steps, explicit reset().
+
+Observation buffers returned by VecMagicalEnv are the simulator's output
+tensors; they are rewritten by the next step (copy them to keep them).
+"""
+import collections
+import ctypes
+
+import numpy as np
+import torch
+
+from . import native, registry, spaces, tables
+
+_LIBRARY = None
+
+
+def library():
+    global _LIBRARY
+    if _LIBRARY is None:
+        _LIBRARY = tables.build_library()
+    return _LIBRARY
+
+
+def _obs_shapes(spec):
+    pp = spec.preproc
+    if pp is None:
+        return collections.OrderedDict([("allo", (384, 384, 3)), ("ego", (384, 384, 3))])
+    if pp == "LoResStack":
+        return collections.OrderedDict([("allo", (96, 96, 12)), ("ego", (96, 96, 12))])
+    cf = registry.PREPROCESSORS[pp]["channels_first"]
+    shapes = collections.OrderedDict([("allo", (96, 96, 3)), ("ego", (96, 96, 3)), ("past_obs", (96, 96, 12))])
+    if cf:
+        shapes = collections.OrderedDict((k, (s[2], s[0], s[1])) for k, s in shapes.items())
+    return shapes
+
+
+def observation_space(spec):
+    return spaces.Dict(collections.OrderedDict(
+        (k, spaces.Box(low=0, high=255, shape=s, dtype=np.uint8)) for k, s in _obs_shapes(spec).items()))
+
+
+class VecMagicalEnv:
+    """Batched MAGICAL env on one MI355X (C ABI: include/magical_sim.h)."""
+
+    def __init__(self, env_name, num_envs, device="cuda:0", seeds=None, base_seed=0, auto_reset=True):
+        self.spec = registry.lookup(env_name)
+        if not self.spec.gpu_supported:
+            raise NotImplementedError(f"{env_name}: task not on the GPU hot path yet")
+        pp = self.spec.preproc
+        if pp in ("LoRes3EA",):
+            raise NotImplementedError(f"{env_name}: preprocessor {pp} not implemented on the GPU path yet")
+        self.num_envs = int(num_envs)
+        self.device = torch.device(device)
+        self.lib = native.load()
+        self._chw = pp is not None and registry.PREPROCESSORS[pp].get("channels_first", False)
+        gpu_pp = {None: 0, "LoRes4E": 1, "LoResStack": 2, "LoRes4A": 4, "LoResCHW4E": 1, "LoResCHW4A": 1}[pp]
+        cfg = native.mg_config()
+        cfg.task = self.spec.task_id
+        cfg.rand_flags = self.spec.rand_flags
+        cfg.preproc = gpu_pp
+        cfg.num_envs = self.num_envs
+        cfg.device = self.device.index or 0
+        cfg.max_episode_steps = self.spec.max_episode_steps
+        cfg.base_seed = base_seed
+        cfg.auto_reset = 1 if auto_reset else 0
+        if seeds is not None:
+            self._seeds = (ctypes.c_uint32 * self.num_envs)(*[int(s) & 0xffffffff for s in seeds])
+            cfg.seeds = self._seeds
+        lib_struct = library()
+        cfg.library = ctypes.cast(ctypes.pointer(lib_struct), ctypes.c_void_p)
+        cfg.library_size = ctypes.sizeof(tables.mg_library)
+        torch.cuda.init()
+        handle = ctypes.c_void_p()
+        native.check(self.lib.mg_create(ctypes.byref(cfg), ctypes.byref(handle)))
+        self.handle = handle
+        n, dev = self.num_envs, self.device
+        u8 = dict(dtype=torch.uint8, device=dev)
+        if pp is None:
+            self.full = torch.empty((n, 2, 384, 384, 3), **u8)
+            self.obs_allo = self.obs_ego = self.obs_past = None
+        elif pp == "LoResStack":
+            self.obs_allo = torch.empty((n, 96, 96, 12), **u8)
+            self.obs_ego = torch.empty((n, 96, 96, 12), **u8)
+            self.obs_past = None
+        else:
+            self.obs_allo = torch.empty((n, 96, 96, 3), **u8)
+            self.obs_ego = torch.empty((n, 96, 96, 3), **u8)
+            self.obs_past = torch.empty((n, 96, 96, 12), **u8)
+        self.reward = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.done = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.eval_score = torch.zeros(n, dtype=torch.float64, device=dev)
+        buf = native.mg_buffers()
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        buf.obs_allo, buf.obs_ego, buf.obs_past = ptr(self.obs_allo), ptr(self.obs_ego), ptr(self.obs_past)
+        buf.reward, buf.done, buf.eval_score = ptr(self.reward), ptr(self.done), ptr(self.eval_score)
+        native.check(self.lib.mg_bind_outputs(self.handle, ctypes.byref(buf)))
+        self.action_space = spaces.Discrete(18)
+        self.observation_space = observation_space(self.spec)
+
+    # -- helpers -----------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _obs(self):
+        if self.spec.preproc is None:
+            return collections.OrderedDict([("allo", self.full[:, 0]), ("ego", self.full[:, 1])])
+        out = collections.OrderedDict([("allo", self.obs_allo), ("ego", self.obs_ego)])
+        if self.obs_past is not None:
+            out["past_obs"] = self.obs_past
+        if self._chw:
+            out = collections.OrderedDict((k, v.permute(0, 3, 1, 2)) for k, v in out.items())
+        return out
+
+    # -- API -----------------------------------------------------------------
+    def seed(self, seeds):
+        arr = (ctypes.c_uint32 * self.num_envs)(*[int(s) & 0xffffffff for s in seeds])
+        native.check(self.lib.mg_seed(self.handle, arr))
+        return list(seeds)
+
+    def reset(self, mask=None):
+        m = None if mask is None else ctypes.c_void_p(mask.to(self.device, torch.uint8).contiguous().data_ptr())
+        native.check(self.lib.mg_reset(self.handle, m, self._stream()))
+        if self.spec.preproc is None:
+            self.render_full(out=self.full)
+        return self._obs()
+
+    def step(self, actions):
+        a = actions
+        if not (isinstance(a, torch.Tensor) and a.dtype == torch.uint8 and a.device == self.device and a.is_contiguous()):
+            a = torch.as_tensor(actions).to(self.device, torch.uint8).contiguous()
+        self._last_actions = a
+        native.check(self.lib.mg_step(self.handle, ctypes.c_void_p(a.data_ptr()), self._stream()))
+        if self.spec.preproc is None:
+            self.render_full(out=self.full)
+        return self._obs(), self.reward, self.done.bool(), {"eval_score": self.eval_score}
+
+    def random_actions(self, step, key=42, out=None):
+        out = out if out is not None else torch.empty(self.num_envs, dtype=torch.uint8, device=self.device)
+        native.check(self.lib.mg_random_actions(self.handle, ctypes.c_void_p(out.data_ptr()), key, step, self._stream()))
+        return out
+
+    def render_full(self, out=None):
+        out = out if out is not None else torch.empty((self.num_envs, 2, 384, 384, 3), dtype=torch.uint8,
+                                                      device=self.device)
+        native.check(self.lib.mg_render_full(self.handle, ctypes.c_void_p(out.data_ptr()), self._stream()))
+        return out
+
+    def bodies(self):
+        out = torch.empty((self.num_envs, 16, 6), dtype=torch.float64, device=self.device)
+        counts = torch.empty((self.num_envs, 4), dtype=torch.int32, device=self.device)
+        native.check(self.lib.mg_get_bodies(self.handle, ctypes.c_void_p(out.data_ptr()),
+                                            ctypes.c_void_p(counts.data_ptr()), self._stream()))
+        return out, counts
+
+    def errors(self):
+        out = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
+        native.check(self.lib.mg_get_errors(self.handle, ctypes.c_void_p(out.data_ptr()), self._stream()))
+        return out
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            self.lib.mg_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MagicalEnv:
+    """Single instance with the reference's gym.Env surface (numpy observations)."""
+
+    metadata = {"render.modes": ["rgb_array"]}
+
+    def __init__(self, env_name, device="cuda:0", seed=None):
+        self.spec = registry.lookup(env_name)
+        self._vec = VecMagicalEnv(env_name, 1, device=device, auto_reset=False)
+        self.max_episode_steps = self.spec.max_episode_steps
+        self.action_space = spaces.Discrete(18)
+        self.observation_space = observation_space(self.spec)
+        self._episode_steps = None
+        self.seed(seed)
+
+    def seed(self, seed=None):
+        """base_env.py:134-141: RandomState(seed); None draws from the global numpy RNG."""
+        if seed is None:
+            seed = np.random.randint(0, (1 << 31) - 1)
+        self._vec.seed([seed])
+        return [seed]
+
+    def action_to_flags(self, int_action):
+        return ACTION_ID_TO_FLAGS[int(int_action)]
+
+    def flags_to_action(self, flags):
+        return FLAGS_TO_ACTION_ID[tuple(flags)]
+
+    def _np_obs(self, obs):
+        return collections.OrderedDict((k, v[0].cpu().numpy()) for k, v in obs.items())
+
+    def reset(self):
+        self._episode_steps = 0
+        return self._np_obs(self._vec.reset())
+
+    def step(self, action):
+        if self._episode_steps is None:
+            raise RuntimeError("call reset() before step()")
+        obs, rew, done, info = self._vec.step(torch.tensor([int(action)], dtype=torch.uint8))
+        self._episode_steps += 1
+        d = bool(done[0].item())
+        score = float(info["eval_score"][0].item())
+        return self._np_obs(obs), float(rew[0].item()), d, {"eval_score": score}
+
+    def render(self, mode="rgb_array"):
+        if mode != "rgb_array":
+            raise NotImplementedError("headless: only rgb_array")
+        full = self._vec.render_full()[0].cpu().numpy()
+        return collections.OrderedDict([("allo", full[0]), ("ego", full[1])])
+
+    def close(self):
+        self._vec.close()
+
+
+# entities.py:148-190
+_UD = [0, 1, 2]            # NONE, UP, DOWN
+_LR = [0, 4, 8]            # NONE, LEFT, RIGHT
+ACTION_NUMS_FLAGS_NAMES = []
+for _aid in range(18):
+    _grip = 16 if _aid < 9 else 32
+    _ud, _lr = _UD[_aid % 3], _LR[(_aid // 3) % 3]
+    _names = {0: "", 1: "Up", 2: "Down"}[_ud] + {0: "", 4: "Left", 8: "Right"}[_lr] + ("Open" if _grip == 16 else "Close")
+    ACTION_NUMS_FLAGS_NAMES.append((_aid, (_ud, _lr, _grip), _names))
+ACTION_ID_TO_FLAGS = {a: f for a, f, _ in ACTION_NUMS_FLAGS_NAMES}
+FLAGS_TO_ACTION_ID = {f: a for a, f, _ in ACTION_NUMS_FLAGS_NAMES}

@@ -1,0 +1,70 @@
+"""ctypes binding of the C ABI (include/magical_sim.h).
+
+The HIP library is the only compute path: if libmagical_sim.so is missing this
+module raises at import time -- there is no CPU fallback.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmagical_sim.so")
+
+EXPORTS = ["mg_create", "mg_bind_outputs", "mg_reset", "mg_step", "mg_render_full", "mg_get_bodies",
+           "mg_get_errors", "mg_seed", "mg_random_actions", "mg_num_envs", "mg_destroy", "mg_last_error"]
+
+
+class mg_config(ctypes.Structure):
+    _fields_ = [("task", ctypes.c_int32), ("rand_flags", ctypes.c_int32), ("preproc", ctypes.c_int32),
+                ("num_envs", ctypes.c_int32), ("device", ctypes.c_int32), ("max_episode_steps", ctypes.c_int32),
+                ("base_seed", ctypes.c_uint32), ("auto_reset", ctypes.c_int32),
+                ("seeds", ctypes.POINTER(ctypes.c_uint32)), ("library", ctypes.c_void_p),
+                ("library_size", ctypes.c_int64)]
+
+
+class mg_buffers(ctypes.Structure):
+    _fields_ = [("obs_allo", ctypes.c_void_p), ("obs_ego", ctypes.c_void_p), ("obs_past", ctypes.c_void_p),
+                ("reward", ctypes.c_void_p), ("done", ctypes.c_void_p), ("eval_score", ctypes.c_void_p)]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load the in-tree HIP library (loud failure if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(f"{LIB_PATH} not found: build it with `python -m magical_amd.build` "
+                          "(no CPU fallback exists for the simulator)")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, i32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64
+    lib.mg_create.argtypes = [ctypes.POINTER(mg_config), ctypes.POINTER(vp)]
+    lib.mg_bind_outputs.argtypes = [vp, ctypes.POINTER(mg_buffers)]
+    lib.mg_reset.argtypes = [vp, vp, vp]
+    lib.mg_step.argtypes = [vp, vp, vp]
+    lib.mg_render_full.argtypes = [vp, vp, vp]
+    lib.mg_get_bodies.argtypes = [vp, vp, vp, vp]
+    lib.mg_get_errors.argtypes = [vp, vp, vp]
+    lib.mg_seed.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
+    lib.mg_random_actions.argtypes = [vp, vp, u64, u64, vp]
+    lib.mg_num_envs.argtypes = [vp]
+    lib.mg_destroy.argtypes = [vp]
+    lib.mg_destroy.restype = None
+    lib.mg_last_error.restype = ctypes.c_char_p
+    for name in EXPORTS[:-2]:
+        if getattr(lib, name).restype is ctypes.c_int:  # default
+            getattr(lib, name).restype = i32
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = _lib.mg_last_error().decode() if _lib is not None else ""
+        raise NativeError(f"magical_sim error {rc}: {msg}")
+    return rc
