@@ -34,6 +34,10 @@ struct mg_sim {
     int task, flags, preproc, max_steps, device, auto_reset;
     mg_buffers out;
     int bound;
+    // optional per-kernel timing (hipEvents on the launch stream)
+    int timing;
+    std::vector<hipEvent_t> ev;   // triples: before step_kernel, between kernels, after render_kernel
+    size_t ev_used;
 };
 
 // ---------------------------------------------------------------------------
@@ -199,6 +203,7 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     HIPC(hipSetDevice(cfg->device));
     mg_sim *s = new mg_sim();
     memset(&s->S, 0, sizeof(MGState));
+    s->timing = 0; s->ev_used = 0; s->bound = 0;
     s->task = cfg->task; s->flags = cfg->rand_flags; s->preproc = cfg->preproc;
     s->max_steps = cfg->max_episode_steps; s->device = cfg->device; s->auto_reset = cfg->auto_reset;
     s->S.n_envs = cfg->num_envs;
@@ -212,7 +217,7 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     Carver real = {(char *)s->pool, 0};
     layout(s->S, real);
     err = hipMalloc((void **)&s->dlib, sizeof(mg_library));
-    if (err != hipSuccess) { hipFree(s->pool); delete s; return set_err(-12, "mg_create: hipMalloc library"); }
+    if (err != hipSuccess) { (void)hipFree(s->pool); delete s; return set_err(-12, "mg_create: hipMalloc library"); }
     HIPC(hipMemcpy(s->dlib, cfg->library, sizeof(mg_library), hipMemcpyHostToDevice));
     std::vector<uint32_t> seeds(cfg->num_envs);
     for (int i = 0; i < cfg->num_envs; i++) seeds[i] = cfg->seeds ? cfg->seeds[i] : cfg->base_seed + (uint32_t)i;
@@ -262,11 +267,17 @@ int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
     HIPC(hipSetDevice(s->device));
     hipStream_t st = as_stream(stream);
     TaskCfg cfg = {s->task, s->flags};
+    hipEvent_t *ev = nullptr;
+    if (s->timing && s->ev_used + 3 <= s->ev.size()) { ev = &s->ev[s->ev_used]; s->ev_used += 3; }
+    if (ev) HIPC(hipEventRecord(ev[0], st));
     hipLaunchKernelGGL(step_kernel, dim3(grid64(s)), dim3(64), 0, st, s->S, s->dlib, cfg, s->max_steps, s->auto_reset, actions,
                        s->out.reward, s->out.done, s->out.eval_score);
     HIPC(hipGetLastError());
-    if (s->preproc != MG_PREPROC_NONE) return render_lores(s, st);
-    return 0;
+    if (ev) HIPC(hipEventRecord(ev[1], st));
+    int rc = 0;
+    if (s->preproc != MG_PREPROC_NONE) rc = render_lores(s, st);
+    if (ev) HIPC(hipEventRecord(ev[2], st));
+    return rc;
 }
 
 int mg_render_full(mg_sim *s, uint8_t *out, void *stream) {
@@ -308,11 +319,43 @@ int mg_random_actions(mg_sim *s, uint8_t *actions, uint64_t key, uint64_t step, 
 
 int mg_num_envs(const mg_sim *s) { return s ? s->S.n_envs : -22; }
 
+int mg_enable_timing(mg_sim *s, int max_steps) {
+    if (!s) return set_err(-22, "mg_enable_timing: null sim");
+    HIPC(hipSetDevice(s->device));
+    for (hipEvent_t e : s->ev) HIPC(hipEventDestroy(e));
+    s->ev.clear();
+    s->ev_used = 0;
+    s->timing = max_steps > 0;
+    for (int i = 0; i < 3 * max_steps; i++) {
+        hipEvent_t e;
+        HIPC(hipEventCreate(&e));
+        s->ev.push_back(e);
+    }
+    return 0;
+}
+
+int mg_read_timing(mg_sim *s, double *out) {
+    if (!s || !out) return set_err(-22, "mg_read_timing: null argument");
+    double t_step = 0.0, t_render = 0.0;
+    int n = (int)(s->ev_used / 3);
+    for (int i = 0; i < n; i++) {
+        float a = 0.f, b = 0.f;
+        HIPC(hipEventSynchronize(s->ev[3 * i + 2]));
+        HIPC(hipEventElapsedTime(&a, s->ev[3 * i], s->ev[3 * i + 1]));
+        HIPC(hipEventElapsedTime(&b, s->ev[3 * i + 1], s->ev[3 * i + 2]));
+        t_step += a; t_render += b;
+    }
+    out[0] = t_step; out[1] = t_render; out[2] = n;
+    s->ev_used = 0;
+    return 0;
+}
+
 void mg_destroy(mg_sim *s) {
     if (!s) return;
-    hipSetDevice(s->device);
-    hipFree(s->pool);
-    hipFree(s->dlib);
+    (void)hipSetDevice(s->device);
+    for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
+    (void)hipFree(s->pool);
+    (void)hipFree(s->dlib);
     delete s;
 }
 

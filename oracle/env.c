@@ -151,3 +151,11 @@ int oenv_get_entities(const OEnv *e, int *kinds, int *types, int *colours, doubl
 }
 
 double oenv_last_score(const OEnv *e) { return e->last_score; }
+
+void oenv_get_phys_vars(const OEnv *e, double out[5]) {
+    for (int i = 0; i < 5; i++) out[i] = e->pv[i];
+}
+
+void o_palette(uint8_t out[5][4][3]) { memcpy(out, O_PALETTE, sizeof(O_PALETTE)); }
+
+void o_downsample(const uint8_t *frame384, uint8_t *out96) { oraster_downsample(frame384, out96); }

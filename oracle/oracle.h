@@ -97,6 +97,12 @@ int oenv_num_arbiters(const OEnv *e);
 /* per-env scene summary for tests: entity kinds/types/colours (returns count) */
 int oenv_get_entities(const OEnv *e, int *kinds, int *types, int *colours, double *poses);
 double oenv_last_score(const OEnv *e);
+/* PhysicsVariables values of the current episode (base_env.py:49-57 order) */
+void oenv_get_phys_vars(const OEnv *e, double out[5]);
+/* palette [colour][base, darken, lighten2, lighten4][rgb] (style.py) */
+void o_palette(uint8_t out[5][4][3]);
+/* cv2 INTER_AREA 384^2 -> 96^2 restatement on an arbitrary frame */
+void o_downsample(const uint8_t *frame384, uint8_t *out96);
 
 #ifdef __cplusplus
 }

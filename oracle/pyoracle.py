@@ -27,8 +27,7 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            build()
+        build()  # make: no-op when up to date
         L = ctypes.CDLL(LIB_PATH)
         d, i, u32, vp = ctypes.c_double, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p
         L.o_crsin.restype = d; L.o_crsin.argtypes = [d]
@@ -59,6 +58,9 @@ def lib():
         L.o_mat3_mul.argtypes = [vp, vp, vp]
         L.o_allo_view.argtypes = [vp]
         L.o_ego_view.argtypes = [d, d, d, vp]
+        L.oenv_get_phys_vars.argtypes = [vp, vp]
+        L.o_palette.argtypes = [vp]
+        L.o_downsample.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -145,6 +147,11 @@ class OracleEnv:
         n = self.L.oenv_get_bodies(self.h, ptr(out), 32)
         return out[:n].copy()
 
+    def phys_vars(self):
+        out = np.zeros(5)
+        self.L.oenv_get_phys_vars(self.h, ptr(out))
+        return out
+
     def num_arbiters(self):
         return self.L.oenv_num_arbiters(self.h)
 
@@ -155,3 +162,17 @@ class OracleEnv:
         p = np.zeros((32, 4))
         n = self.L.oenv_get_entities(self.h, ptr(k), ptr(t), ptr(c), ptr(p))
         return k[:n].copy(), t[:n].copy(), c[:n].copy(), p[:n].copy()
+
+
+def palette():
+    out = np.zeros((5, 4, 3), dtype=np.uint8)
+    lib().o_palette(ptr(out))
+    return out
+
+
+def downsample(frame):
+    frame = np.ascontiguousarray(frame, dtype=np.uint8)
+    assert frame.shape == (384, 384, 3)
+    out = np.zeros((96, 96, 3), dtype=np.uint8)
+    lib().o_downsample(ptr(frame), ptr(out))
+    return out

@@ -101,3 +101,38 @@ def test_full_resolution_frames(name):
                 assert np.array_equal(full[i, 0], a), f"allo frame step {t} env {i}"
                 assert np.array_equal(full[i, 1], g), f"ego frame step {t} env {i}"
     vec.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n,steps", [("MoveToRegion-Demo-LoRes4E-v0", 4096, 45),
+                                          ("MatchRegions-TestAll-LoRes4E-v0", 8192, 20)])
+def test_full_size_sampled_parity(name, n, steps):
+    """BASELINE sizes: every env steps on the GPU, a spread of envs (incl. the
+    first/last lanes of 64-wide blocks and the last env) is checked bit-exact
+    against the oracle, across an auto-reset boundary for MoveToRegion (40)."""
+    spec = registry.lookup(name)
+    seeds = [1000 + i for i in range(n)]
+    vec = magical_amd.make_vec(name, n, seeds=seeds)
+    pick = sorted({0, 1, 63, 64, 127, n // 2 + 5, n - 65, n - 1})
+    orc = {i: oracle_env(spec, seeds[i]) for i in pick}
+    acts = np.random.RandomState(9).randint(0, 18, (steps, n))
+    obs = vec.reset()
+    for i in pick:
+        ref = oracle_obs_split(spec, orc[i].reset())
+        for k in obs:
+            assert np.array_equal(obs[k][i].cpu().numpy(), ref[k]), f"reset env {i} {k}"
+    for t in range(steps):
+        obs, rew, done, info = vec.step(torch.as_tensor(acts[t], dtype=torch.uint8))
+        got = {k: v[pick].cpu().numpy() for k, v in obs.items()}
+        got_done = done[pick].cpu().numpy()
+        got_score = info["eval_score"][pick].cpu().numpy()
+        for j, i in enumerate(pick):
+            o, r, d, s = orc[i].step(int(acts[t, i]))
+            assert bool(got_done[j]) == d and got_score[j] == s, f"step {t} env {i}"
+            if d:
+                o = orc[i].reset()
+            ref = oracle_obs_split(spec, o)
+            for k in got:
+                assert np.array_equal(got[k][j], ref[k]), f"step {t} env {i} obs {k}"
+    assert int(vec.errors().abs().sum().item()) == 0
+    vec.close()
