@@ -13,35 +13,53 @@
 #include "mg_step.h"
 
 #define RG_MAXG 160
-#define RG_MAXVERT 2600
+#define RG_MAXVERT 2048
 #define RG_MAXSPAN 6144
-#define RG_MAXLINE 1400
+#define RG_MAXDASH 512
 #define RG_BAND 8
 #define RG_THREADS 256
+#define RG_LOROW (MG_LORES * 3)         // bytes of one 96-px RGB row
+#define RG_BANDLO (2 * RG_LOROW)        // bytes of the 2 LoRes rows one band produces
+#define RG_BANDLO16 (RG_BANDLO / 16)    // ... in 16-byte chunks (36)
 
 struct RenderOut {
     uint8_t *full;      // [N][2][384][384][3] (full-resolution mode) or null
     uint8_t *obs_allo;  // LoRes outputs (layout per preproc), or null
     uint8_t *obs_ego;
     uint8_t *obs_past;
+    const uint8_t *mask;  // reset mask: envs with mask[e] == 0 are left untouched (null: all)
     int preproc;
 };
 
+// LDS: the setup stages (matrices) and the band stages (band buffer + LoRes
+// staging) never live at the same time, so they share storage.
 struct RenderSmem {
-    double g_m[RG_MAXG][6];
-    double e_xf[MG_MAX_ENTS][5][9];
-    double view[9];
-    int16_t g_rpoly[RG_MAXG];
+    union {
+        struct {
+            double g_m[RG_MAXG][6];
+            double e_xf[MG_MAX_ENTS][5][9];
+            double view[9];
+        } pre;
+        struct {
+            uint32_t band[RG_BAND][MG_RES];
+            uint4 lo[RG_BANDLO16];          // current frame, 2 LoRes rows
+            uint4 past[3][RG_BANDLO16];     // frames t-3, t-2, t-1 of the same rows
+        } post;
+    } u;
+    int16_t g_rpoly[RG_MAXG], g_voff[RG_MAXG], g_nv[RG_MAXG];
+    int16_t g_ymin[RG_MAXG], g_ymax[RG_MAXG], g_xmin[RG_MAXG], g_xmax[RG_MAXG];
     int8_t g_ent[RG_MAXG];
-    int16_t g_voff[RG_MAXG], g_ymin[RG_MAXG], g_ymax[RG_MAXG], g_xmin[RG_MAXG], g_xmax[RG_MAXG];
-    int32_t g_soff[RG_MAXG];
-    int16_t vx[RG_MAXVERT], vy[RG_MAXVERT];
+    int32_t g_soff[RG_MAXG + 1];
+    int16_t e_g0[MG_MAX_ENTS + 1];
+    int16_t vx[RG_MAXVERT], vy[RG_MAXVERT];   // int pixel vertices (fill, line ends)
+    int16_t fx[RG_MAXVERT], fy[RG_MAXVERT];   // float->int first points of solid outline edges
+    uint8_t v_geom[RG_MAXVERT];
+    int16_t sedge[RG_MAXVERT];                // solid outline edges (start vertex)
     int16_t span_l[RG_MAXSPAN], span_r[RG_MAXSPAN];
-    int16_t line[RG_MAXLINE][4];
-    int16_t line_o[RG_MAXLINE];
-    uint32_t band[RG_BAND][MG_RES];
+    int16_t dash[RG_MAXDASH][4];              // clipped dashed-outline lines
+    int16_t dash_o[RG_MAXDASH];
     uint32_t col[2 * RG_MAXG + 2];
-    int32_t ngeom, nvert, nspan, nline, err;
+    int32_t ngeom, nvert, nspan, nsedge, ndash, err;
 };
 
 MG_DEV uint32_t pack_rgb(const uint8_t *c) { return (uint32_t)c[0] | ((uint32_t)c[1] << 8) | ((uint32_t)c[2] << 16); }
@@ -90,10 +108,10 @@ MG_DEV bool clipline(int &x1, int &y1, int &x2, int &y2) {
 
 MG_DEV void push_line(RenderSmem &sm, int x1, int y1, int x2, int y2, int ord) {
     if (!clipline(x1, y1, x2, y2)) return;
-    int i = atomicAdd(&sm.nline, 1);
-    if (i >= RG_MAXLINE) { sm.err = 1; return; }
-    sm.line[i][0] = (int16_t)x1; sm.line[i][1] = (int16_t)y1; sm.line[i][2] = (int16_t)x2; sm.line[i][3] = (int16_t)y2;
-    sm.line_o[i] = (int16_t)ord;
+    int i = atomicAdd(&sm.ndash, 1);
+    if (i >= RG_MAXDASH) { sm.err = 1; return; }
+    sm.dash[i][0] = (int16_t)x1; sm.dash[i][1] = (int16_t)y1; sm.dash[i][2] = (int16_t)x2; sm.dash[i][3] = (int16_t)y2;
+    sm.dash_o[i] = (int16_t)ord;
 }
 
 // clip_and_draw_line_width (pygame 1.9.6): base line + offsets 1, -1, 2, ...
@@ -149,13 +167,11 @@ MG_DEV void push_dashes(RenderSmem &sm, double x1, double y1, double x2, double 
 
 MG_DEV void band_put(RenderSmem &sm, int x, int y, int y0, uint32_t ord) {
     int r = y - y0;
-    if (r >= 0 && r < RG_BAND && x >= 0 && x < MG_RES) atomicMax(&sm.band[r][x], ord);
+    if (r >= 0 && r < RG_BAND && x >= 0 && x < MG_RES) atomicMax(&sm.u.post.band[r][x], ord);
 }
 
-// all pixels of a clipped line within rows [y0, y0 + RG_BAND)
-MG_DEV void raster_line_band(RenderSmem &sm, int i, int y0) {
-    int x1 = sm.line[i][0], y1 = sm.line[i][1], x2 = sm.line[i][2], y2 = sm.line[i][3];
-    uint32_t ord = (uint32_t)sm.line_o[i];
+// all pixels of a clipped line (pygame drawline) within rows [y0, y0 + RG_BAND)
+MG_DEV void raster_line_band(RenderSmem &sm, int x1, int y1, int x2, int y2, uint32_t ord, int y0) {
     int y1b = y0 + RG_BAND - 1;
     if (y1 == y2) {
         if (y1 < y0 || y1 > y1b) return;
@@ -193,6 +209,12 @@ MG_DEV void raster_line_band(RenderSmem &sm, int i, int y0) {
     }
 }
 
+// one sub-line of a width-2 outline: clip (pygame clipline) then raster in band
+MG_DEV void clip_raster_band(RenderSmem &sm, int x1, int y1, int x2, int y2, uint32_t ord, int y0) {
+    if (!clipline(x1, y1, x2, y2)) return;
+    raster_line_band(sm, x1, y1, x2, y2, ord, y0);
+}
+
 // render polygon point i (local coordinates); the goal rect is make_rect(w, h) of its entity
 MG_DEV void rpoly_pt(const MGState &S, const mg_library *L, int e, const mg_rpoly &rp, int ent, int i, double &x, double &y) {
     if (rp.pts_off >= 0) { x = L->rpts[rp.pts_off + i][0]; y = L->rpts[rp.pts_off + i][1]; return; }
@@ -225,39 +247,28 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
                                                             int mode) {
     __shared__ RenderSmem sm;
     const int e = blockIdx.x, view = blockIdx.y, tid = threadIdx.x;
-    if (e >= S.n_envs) return;
+    if (e >= S.n_envs || (out.mask && !out.mask[e])) return;
     const int nents = S.nents[e];
     // ---- 1. geometry list (entity add order x render polys), colour table, view ----
-    if (tid == 0) {
-        int g = 0, nv = 0;
-        sm.err = 0; sm.nline = 0;
-        sm.col[0] = pack_rgb(L->background);
-        for (int ent = 0; ent < nents; ent++) {
-            int kind = AT(S.ekind, ent), r0, nr;
-            if (kind == MG_ENT_ARENA) { r0 = L->arena_rpoly0; nr = L->arena_nrpoly; }
-            else if (kind == MG_ENT_GOAL) { r0 = L->goal_rpoly0; nr = L->goal_nrpoly; }
-            else if (kind == MG_ENT_ROBOT) { r0 = L->robot_rpoly0; nr = L->robot_nrpoly; }
-            else { int t = AT(S.etype, ent); r0 = L->block_rpoly0[t]; nr = L->block_nrpoly[t]; }
-            int ecol = AT(S.ecol, ent);
-            for (int k = 0; k < nr && g < RG_MAXG; k++, g++) {
-                const mg_rpoly &rp = L->rpoly[r0 + k];
-                sm.g_rpoly[g] = (int16_t)(r0 + k);
-                sm.g_ent[g] = (int8_t)ent;
-                sm.g_voff[g] = (int16_t)nv;
-                nv += rp.npts;
-                sm.col[2 * g + 1] = ref_colour(L, rp.col_ref, ecol);
-                sm.col[2 * g + 2] = rp.outline ? ref_colour(L, rp.ocol_ref, ecol) : 0u;
-            }
-        }
-        sm.ngeom = g;
-        sm.nvert = nv;
-        if (nv > RG_MAXVERT) sm.err = 2;
-        if (view == 0) { // Viewer.render: stack.push(self.transform) -> eye(3) @ view
-            const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-            mg_mat3_mul(I3, L->allo_view, sm.view);
-        }
+    int my_r0 = 0, my_nr = 0;
+    if (tid < nents) {
+        int kind = AT(S.ekind, tid);
+        if (kind == MG_ENT_ARENA) { my_r0 = L->arena_rpoly0; my_nr = L->arena_nrpoly; }
+        else if (kind == MG_ENT_GOAL) { my_r0 = L->goal_rpoly0; my_nr = L->goal_nrpoly; }
+        else if (kind == MG_ENT_ROBOT) { my_r0 = L->robot_rpoly0; my_nr = L->robot_nrpoly; }
+        else { int t = AT(S.etype, tid); my_r0 = L->block_rpoly0[t]; my_nr = L->block_nrpoly[t]; }
+        sm.e_g0[tid + 1] = (int16_t)my_nr;
     }
-    if (view == 1 && tid == 1) {
+    if (tid == 0) {
+        sm.err = 0; sm.ndash = 0; sm.nsedge = 0;
+        sm.col[0] = pack_rgb(L->background);
+        sm.e_g0[0] = 0;
+    }
+    if (view == 0 && tid == 32) { // Viewer.render: stack.push(self.transform) -> eye(3) @ view
+        const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        mg_mat3_mul(I3, L->allo_view, sm.u.pre.view);
+    }
+    if (view == 1 && tid == 32) {
         // Viewer.set_cam_follow / ego_cam_matrix: P @ (scale @ (tr1 @ (rot @ tr2)))
         int rb = S.robot_body0[e];
         double rot[9], tr2[9], m1[9], m2[9], m3[9];
@@ -268,126 +279,158 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         mg_mat3_mul(L->ego_scale_m, m2, m3);
         mg_mat3_mul(L->pygame_m, m3, m1);
         const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-        mg_mat3_mul(I3, m1, sm.view);
+        mg_mat3_mul(I3, m1, sm.u.pre.view);
     }
-    if (tid < nents) entity_xforms(S, e, tid, sm.e_xf[tid]);
+    if (tid >= 64 && tid - 64 < nents) entity_xforms(S, e, tid - 64, sm.u.pre.e_xf[tid - 64]);
     __syncthreads();
+    if (tid == 0) {
+        for (int k = 0; k < nents; k++) sm.e_g0[k + 1] += sm.e_g0[k];
+        sm.ngeom = sm.e_g0[nents];
+        if (sm.ngeom > RG_MAXG) sm.err = 2;
+    }
+    __syncthreads();
+    if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
     const int G = sm.ngeom;
-    if (sm.err) return;
+    if (tid < nents) {
+        int ecol = AT(S.ecol, tid);
+        for (int k = 0, g = sm.e_g0[tid]; k < my_nr; k++, g++) {
+            const mg_rpoly &rp = L->rpoly[my_r0 + k];
+            sm.g_rpoly[g] = (int16_t)(my_r0 + k);
+            sm.g_ent[g] = (int8_t)tid;
+            sm.g_nv[g] = (int16_t)rp.npts;
+            sm.col[2 * g + 1] = ref_colour(L, rp.col_ref, ecol);
+            sm.col[2 * g + 2] = rp.outline ? ref_colour(L, rp.ocol_ref, ecol) : 0u;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int nv = 0;
+        for (int g = 0; g < G; g++) { sm.g_voff[g] = (int16_t)nv; nv += sm.g_nv[g]; }
+        sm.nvert = nv;
+        if (nv > RG_MAXVERT) sm.err = 2;
+    }
     // ---- 2. per-geom matrix: view @ T_last @ ... @ T_first (Geom.render stack) ----
     for (int g = tid; g < G; g += RG_THREADS) {
         const mg_rpoly &rp = L->rpoly[sm.g_rpoly[g]];
         int ent = sm.g_ent[g];
         double M[9];
-        for (int i = 0; i < 9; i++) M[i] = sm.view[i];
+        for (int i = 0; i < 9; i++) M[i] = sm.u.pre.view[i];
         for (int k = rp.nxf - 1; k >= 0; k--) {
             int x = rp.xf[k];
-            const double *T = x >= MG_XF_STATIC0 ? L->static_xf[x - MG_XF_STATIC0] : sm.e_xf[ent][x];
+            const double *T = x >= MG_XF_STATIC0 ? L->static_xf[x - MG_XF_STATIC0] : sm.u.pre.e_xf[ent][x];
             mg_mat3_mul(M, T, M);
         }
-        for (int i = 0; i < 6; i++) sm.g_m[g][i] = M[i];
+        for (int i = 0; i < 6; i++) sm.u.pre.g_m[g][i] = M[i];
     }
     __syncthreads();
-    // ---- 3. vertices -> int pixel coordinates (pygame (int) truncation) ----
-    for (int g = 0; g < G; g++) {
+    if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
+    const int NV = sm.nvert;
+    for (int g = tid; g < G; g += RG_THREADS)
+        for (int i = 0, v0 = sm.g_voff[g]; i < sm.g_nv[g]; i++) sm.v_geom[v0 + i] = (uint8_t)g;
+    __syncthreads();
+    // ---- 3. vertices -> int pixel coordinates (pygame (int) truncation); outline edges ----
+    for (int v = tid; v < NV; v += RG_THREADS) {
+        int g = sm.v_geom[v], i = v - sm.g_voff[g];
         const mg_rpoly &rp = L->rpoly[sm.g_rpoly[g]];
-        for (int i = tid; i < rp.npts; i += RG_THREADS) {
-            double x, y;
-            rpoly_pt(S, L, e, rp, sm.g_ent[g], i, x, y);
-            const double *M = sm.g_m[g];
-            double gx = __fma_rn(M[1], y, M[0] * x) + M[2];
-            double gy = __fma_rn(M[4], y, M[3] * x) + M[5];
-            sm.vx[sm.g_voff[g] + i] = (int16_t)(int)gx;
-            sm.vy[sm.g_voff[g] + i] = (int16_t)(int)gy;
+        double x, y;
+        rpoly_pt(S, L, e, rp, sm.g_ent[g], i, x, y);
+        const double *M = sm.u.pre.g_m[g];
+        double gx = __fma_rn(M[1], y, M[0] * x) + M[2];
+        double gy = __fma_rn(M[4], y, M[3] * x) + M[5];
+        sm.vx[v] = (int16_t)(int)gx;
+        sm.vy[v] = (int16_t)(int)gy;
+        if (rp.outline == MG_OUTLINE_SOLID) {
+            // lines(): first point via float (pg FloatFromObj), second via int
+            sm.fx[v] = (int16_t)(int)(float)gx;
+            sm.fy[v] = (int16_t)(int)(float)gy;
+            sm.sedge[atomicAdd(&sm.nsedge, 1)] = (int16_t)v;
+        } else if (rp.outline == MG_OUTLINE_DASHED) {
+            int j = i + 1 == rp.npts ? 0 : i + 1;
+            double xb, yb;
+            rpoly_pt(S, L, e, rp, sm.g_ent[g], j, xb, yb);
+            double gxb = __fma_rn(M[1], yb, M[0] * xb) + M[2], gyb = __fma_rn(M[4], yb, M[3] * xb) + M[5];
+            push_dashes(sm, gx, gy, gxb, gyb, 2 * g + 2);
         }
     }
     __syncthreads();
     // ---- 4. per-geom bounding rows / columns; span table offsets ----
-    if (tid == 0) {
-        int off = 0;
-        for (int g = 0; g < G; g++) {
-            const mg_rpoly &rp = L->rpoly[sm.g_rpoly[g]];
-            int v0 = sm.g_voff[g];
-            int ymin = sm.vy[v0], ymax = ymin, xmin = sm.vx[v0], xmax = xmin;
-            for (int i = 1; i < rp.npts; i++) {
-                int y = sm.vy[v0 + i], x = sm.vx[v0 + i];
-                ymin = y < ymin ? y : ymin; ymax = y > ymax ? y : ymax;
-                xmin = x < xmin ? x : xmin; xmax = x > xmax ? x : xmax;
-            }
-            sm.g_ymin[g] = (int16_t)ymin; sm.g_ymax[g] = (int16_t)ymax;
-            sm.g_xmin[g] = (int16_t)(xmin > 0 ? xmin : 0);
-            sm.g_xmax[g] = (int16_t)(xmax < MG_RES - 1 ? xmax : MG_RES - 1);
-            int r0 = ymin > 0 ? ymin : 0, r1 = ymax < MG_RES - 1 ? ymax : MG_RES - 1;
-            sm.g_soff[g] = off;
-            if (r1 >= r0) off += r1 - r0 + 1;
+    for (int g = tid; g < G; g += RG_THREADS) {
+        int v0 = sm.g_voff[g], n = sm.g_nv[g];
+        int ymin = sm.vy[v0], ymax = ymin, xmin = sm.vx[v0], xmax = xmin;
+        for (int i = 1; i < n; i++) {
+            int y = sm.vy[v0 + i], x = sm.vx[v0 + i];
+            ymin = y < ymin ? y : ymin; ymax = y > ymax ? y : ymax;
+            xmin = x < xmin ? x : xmin; xmax = x > xmax ? x : xmax;
         }
-        sm.nspan = off;
-        if (off > RG_MAXSPAN) sm.err = 3;
-    }
-    __syncthreads();
-    if (sm.err) return;
-    // ---- 5. fill spans: pygame draw_fillpoly intersections per row (2 per row for these convex polys) ----
-    for (int g = 0; g < G; g++) {
-        const mg_rpoly &rp = L->rpoly[sm.g_rpoly[g]];
-        int ymin = sm.g_ymin[g], ymax = sm.g_ymax[g];
+        sm.g_ymin[g] = (int16_t)ymin; sm.g_ymax[g] = (int16_t)ymax;
+        sm.g_xmin[g] = (int16_t)(xmin > 0 ? xmin : 0);
+        sm.g_xmax[g] = (int16_t)(xmax < MG_RES - 1 ? xmax : MG_RES - 1);
         int r0 = ymin > 0 ? ymin : 0, r1 = ymax < MG_RES - 1 ? ymax : MG_RES - 1;
-        int v0 = sm.g_voff[g], n = rp.npts;
-        for (int y = r0 + tid; y <= r1; y += RG_THREADS) {
-            int lo = 32767, hi = -32768, cnt = 0;
-            for (int i = 0; i < n; i++) {
-                int ip = i ? i - 1 : n - 1;
-                int ya = sm.vy[v0 + ip], yb = sm.vy[v0 + i], xa, xb;
-                if (ya < yb) { xa = sm.vx[v0 + ip]; xb = sm.vx[v0 + i]; }
-                else if (ya > yb) { int t = ya; ya = yb; yb = t; xa = sm.vx[v0 + i]; xb = sm.vx[v0 + ip]; }
-                else continue;
-                if ((y >= ya && y < yb) || (y == ymax && y > ya && y <= yb)) {
-                    int x = (y - ya) * (xb - xa) / (yb - ya) + xa;
-                    lo = x < lo ? x : lo; hi = x > hi ? x : hi;
-                    cnt++;
-                }
-            }
-            if (cnt != 0 && cnt != 2) sm.err = 4;
-            if (cnt == 0) { lo = 32767; hi = -32768; }
-            sm.span_l[sm.g_soff[g] + y - r0] = (int16_t)lo;
-            sm.span_r[sm.g_soff[g] + y - r0] = (int16_t)hi;
-        }
-    }
-    // ---- 6. outline line list: solid width 2 (pygame.draw.lines) and dashed width 4 ----
-    for (int g = 0; g < G; g++) {
-        const mg_rpoly &rp = L->rpoly[sm.g_rpoly[g]];
-        if (rp.outline == MG_OUTLINE_NONE) continue;
-        int n = rp.npts, v0 = sm.g_voff[g];
-        const double *M = sm.g_m[g];
-        for (int i = tid; i < n; i += RG_THREADS) {
-            int j = (i + 1) % n;
-            double xa, ya;
-            rpoly_pt(S, L, e, rp, sm.g_ent[g], i, xa, ya);
-            double gxa = __fma_rn(M[1], ya, M[0] * xa) + M[2], gya = __fma_rn(M[4], ya, M[3] * xa) + M[5];
-            if (rp.outline == MG_OUTLINE_SOLID) {
-                // lines(): first point via float (pg FloatFromObj), second via int
-                push_wide_line(sm, (int)(float)gxa, (int)(float)gya, sm.vx[v0 + j], sm.vy[v0 + j], 2, 2 * g + 2);
-            } else {
-                double xb, yb;
-                rpoly_pt(S, L, e, rp, sm.g_ent[g], j, xb, yb);
-                double gxb = __fma_rn(M[1], yb, M[0] * xb) + M[2], gyb = __fma_rn(M[4], yb, M[3] * xb) + M[5];
-                push_dashes(sm, gxa, gya, gxb, gyb, 2 * g + 2);
-            }
-        }
+        sm.g_soff[g + 1] = r1 >= r0 ? r1 - r0 + 1 : 0;
     }
     __syncthreads();
-    if (sm.err) {
-        if (tid == 0) S.overflow[e] |= 4 << view;
-        return;
+    if (tid == 0) {
+        sm.g_soff[0] = 0;
+        for (int g = 0; g < G; g++) sm.g_soff[g + 1] += sm.g_soff[g];
+        sm.nspan = sm.g_soff[G];
+        if (sm.nspan > RG_MAXSPAN) sm.err = 3;
     }
-    const int nline = sm.nline < RG_MAXLINE ? sm.nline : RG_MAXLINE;
-    // ---- 7. bands ----
+    __syncthreads();
+    if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
+    // ---- 5. fill spans: pygame draw_fillpoly intersections per row (2 per row for these convex polys) ----
+    for (int s = tid; s < sm.nspan; s += RG_THREADS) {
+        int lo_g = 0, hi_g = G - 1; // last g with g_soff[g] <= s
+        while (lo_g < hi_g) {
+            int mid = (lo_g + hi_g + 1) >> 1;
+            if (sm.g_soff[mid] <= s) lo_g = mid; else hi_g = mid - 1;
+        }
+        const int g = lo_g;
+        int ymin = sm.g_ymin[g], ymax = sm.g_ymax[g];
+        int y = (ymin > 0 ? ymin : 0) + s - sm.g_soff[g];
+        int v0 = sm.g_voff[g], n = sm.g_nv[g];
+        int lo = 32767, hi = -32768, cnt = 0;
+        for (int i = 0; i < n; i++) {
+            int ip = i ? i - 1 : n - 1;
+            int ya = sm.vy[v0 + ip], yb = sm.vy[v0 + i], xa, xb;
+            if (ya < yb) { xa = sm.vx[v0 + ip]; xb = sm.vx[v0 + i]; }
+            else if (ya > yb) { int t = ya; ya = yb; yb = t; xa = sm.vx[v0 + i]; xb = sm.vx[v0 + ip]; }
+            else continue;
+            if ((y >= ya && y < yb) || (y == ymax && y > ya && y <= yb)) {
+                int x = (y - ya) * (xb - xa) / (yb - ya) + xa;
+                lo = x < lo ? x : lo; hi = x > hi ? x : hi;
+                cnt++;
+            }
+        }
+        if (cnt != 0 && cnt != 2) sm.err = 4;
+        if (cnt == 0) { lo = 32767; hi = -32768; }
+        sm.span_l[s] = (int16_t)lo;
+        sm.span_r[s] = (int16_t)hi;
+    }
+    __syncthreads();
+    if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
+    const int ndash = sm.ndash, nsedge = sm.nsedge;
+    // ---- 6. bands ----
     uint8_t *ring = view == 0 ? S.hist_allo : S.hist_ego;
     const size_t FR = (size_t)MG_LORES * MG_LORES * 3;
     const bool fresh = S.episode_steps[e] == 0;
     const int head = S.hist_head[view * S.N + e];
     const int nh = fresh ? 0 : ((head + 1) & 3);
+    const int pp = out.preproc;
+    const bool stacked = pp == MG_PREPROC_LORESSTACK || (pp == MG_PREPROC_LORES4E && view == 1) ||
+                         (pp == MG_PREPROC_LORES4A && view == 0);
+    const bool plain = pp != MG_PREPROC_LORESSTACK;   // the view's own current-frame output
+    uint8_t *o_plain = view == 0 ? out.obs_allo : out.obs_ego;
+    uint8_t *o_stack = pp == MG_PREPROC_LORESSTACK ? o_plain : out.obs_past;
     for (int y0 = 0; y0 < MG_RES; y0 += RG_BAND) {
-        for (int i = tid; i < RG_BAND * MG_RES; i += RG_THREADS) (&sm.band[0][0])[i] = 0u;
+        const size_t lrow = (size_t)(y0 / 4) * RG_LOROW;  // byte offset of this band's LoRes rows
+        // prefetch frames t-3..t-1 of these rows (ring slots nh+1..nh+3, never written this step)
+        uint4 pf = make_uint4(0, 0, 0, 0);
+        const bool do_pf = mode == 0 && stacked && !fresh && tid < 3 * RG_BANDLO16;
+        if (do_pf) {
+            int k = tid / RG_BANDLO16, c = tid % RG_BANDLO16, sl = (nh + 1 + k) & 3;
+            pf = *(const uint4 *)(ring + ((size_t)sl * S.N + e) * FR + lrow + 16 * c);
+        }
+        for (int i = tid; i < RG_BAND * MG_RES; i += RG_THREADS) (&sm.u.post.band[0][0])[i] = 0u;
         __syncthreads();
         for (int g = 0; g < G; g++) {
             int ymin = sm.g_ymin[g], ymax = sm.g_ymax[g];
@@ -401,62 +444,75 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             for (int i = tid; i < total; i += RG_THREADS) {
                 int y = ra + i / w, x = xmin + i % w;
                 int s = sm.g_soff[g] + y - r0;
-                if (x >= sm.span_l[s] && x <= sm.span_r[s]) atomicMax(&sm.band[y - y0][x], ord);
+                if (x >= sm.span_l[s] && x <= sm.span_r[s]) atomicMax(&sm.u.post.band[y - y0][x], ord);
             }
         }
-        for (int i = tid; i < nline; i += RG_THREADS) raster_line_band(sm, i, y0);
+        // solid width-2 outlines (clip_and_draw_line_width: base line + one offset copy)
+        for (int k = tid; k < nsedge; k += RG_THREADS) {
+            int v = sm.sedge[k], g = sm.v_geom[v];
+            int nx = v + 1 == sm.g_voff[g] + sm.g_nv[g] ? sm.g_voff[g] : v + 1;
+            int x1 = sm.fx[v], y1 = sm.fy[v], x2 = sm.vx[nx], y2 = sm.vy[nx];
+            int ylo = (y1 < y2 ? y1 : y2) - 1, yhi = (y1 > y2 ? y1 : y2) + 1;
+            if (yhi < y0 || ylo >= y0 + RG_BAND) continue;
+            uint32_t ord = 2 * g + 2;
+            clip_raster_band(sm, x1, y1, x2, y2, ord, y0);
+            if (abs(x1 - x2) > abs(y1 - y2)) clip_raster_band(sm, x1, y1 + 1, x2, y2 + 1, ord, y0);
+            else clip_raster_band(sm, x1 + 1, y1, x2 + 1, y2, ord, y0);
+        }
+        for (int i = tid; i < ndash; i += RG_THREADS)
+            raster_line_band(sm, sm.dash[i][0], sm.dash[i][1], sm.dash[i][2], sm.dash[i][3], (uint32_t)sm.dash_o[i], y0);
         __syncthreads();
         if (mode == 1) {
             uint8_t *dst = out.full + (((size_t)e * 2 + view) * MG_RES + y0) * MG_RES * 3;
             for (int i = tid; i < RG_BAND * MG_RES; i += RG_THREADS) {
-                uint32_t c = sm.col[(&sm.band[0][0])[i]];
+                uint32_t c = sm.col[(&sm.u.post.band[0][0])[i]];
                 dst[3 * i] = (uint8_t)(c & 255); dst[3 * i + 1] = (uint8_t)((c >> 8) & 255); dst[3 * i + 2] = (uint8_t)(c >> 16);
             }
-        } else {
-            for (int t = tid; t < (RG_BAND / 4) * MG_LORES; t += RG_THREADS) {
-                int oyl = t / MG_LORES, ox = t % MG_LORES, oy = y0 / 4 + oyl;
-                int sr = 0, sg = 0, sb = 0;
-                for (int dy = 0; dy < 4; dy++)
-                    for (int dx = 0; dx < 4; dx++) {
-                        uint32_t c = sm.col[sm.band[oyl * 4 + dy][ox * 4 + dx]];
-                        sr += c & 255; sg += (c >> 8) & 255; sb += c >> 16;
-                    }
-                uint8_t px[3];
-                int ss[3] = {sr, sg, sb};
-                for (int ch = 0; ch < 3; ch++) {
-                    int q = ss[ch] >> 4, r = ss[ch] & 15;
-                    px[ch] = (uint8_t)(q + (r > 8 || (r == 8 && (q & 1))));
+            __syncthreads();
+            continue;
+        }
+        // 4x4 area downsample (round half to even of sum/16) into LDS staging
+        uint8_t *lo8 = (uint8_t *)sm.u.post.lo;
+        for (int t = tid; t < (RG_BAND / 4) * MG_LORES; t += RG_THREADS) {
+            int oyl = t / MG_LORES, ox = t % MG_LORES;
+            int sr = 0, sg = 0, sb = 0;
+            for (int dy = 0; dy < 4; dy++)
+                for (int dx = 0; dx < 4; dx++) {
+                    uint32_t c = sm.col[sm.u.post.band[oyl * 4 + dy][ox * 4 + dx]];
+                    sr += c & 255; sg += (c >> 8) & 255; sb += c >> 16;
                 }
-                size_t pix = (size_t)oy * MG_LORES + ox;
-                // ring of the last 4 downsampled frames of this view
-                if (fresh) {
-                    for (int s = 0; s < 4; s++)
-                        for (int ch = 0; ch < 3; ch++) ring[((size_t)s * S.N + e) * FR + pix * 3 + ch] = px[ch];
-                } else {
-                    for (int ch = 0; ch < 3; ch++) ring[((size_t)nh * S.N + e) * FR + pix * 3 + ch] = px[ch];
+            int ss[3] = {sr, sg, sb};
+            for (int ch = 0; ch < 3; ch++) {
+                int q = ss[ch] >> 4, r = ss[ch] & 15;
+                lo8[t * 3 + ch] = (uint8_t)(q + (r > 8 || (r == 8 && (q & 1))));
+            }
+        }
+        if (do_pf) sm.u.post.past[tid / RG_BANDLO16][tid % RG_BANDLO16] = pf;
+        __syncthreads();
+        // ring of the last 4 LoRes frames: slot nh (all 4 slots at episode start)
+        for (int t = tid; t < (fresh ? 4 : 1) * RG_BANDLO16; t += RG_THREADS) {
+            int sl = fresh ? t / RG_BANDLO16 : nh, c = t % RG_BANDLO16;
+            *(uint4 *)(ring + ((size_t)sl * S.N + e) * FR + lrow + 16 * c) = sm.u.post.lo[c];
+        }
+        if (plain)
+            for (int c = tid; c < RG_BANDLO16; c += RG_THREADS)
+                *(uint4 *)(o_plain + (size_t)e * FR + lrow + 16 * c) = sm.u.post.lo[c];
+        if (stacked) {
+            // FlattenFrameStack: [96][96][12] = frames oldest..newest concatenated per pixel
+            const uint8_t *p8 = (const uint8_t *)sm.u.post.past;
+            for (int c = tid; c < 4 * RG_BANDLO16; c += RG_THREADS) {
+                uint8_t b[16];
+                for (int j = 0; j < 16; j++) {
+                    int byte = 16 * c + j, px = byte / 12, k = (byte % 12) / 3, ch = byte % 3;
+                    int src = px * 3 + ch;
+                    b[j] = (k == 3 || fresh) ? lo8[src] : p8[k * RG_BANDLO + src];
                 }
-                // frames oldest..newest: slots nh-3 .. nh
-                const int pp = out.preproc;
-                uint8_t *o1 = view == 0 ? out.obs_allo : out.obs_ego;
-                if (pp == MG_PREPROC_LORESSTACK) {
-                    for (int k = 0; k < 4; k++) {
-                        int s = (nh + 1 + k) & 3;
-                        for (int ch = 0; ch < 3; ch++)
-                            o1[((size_t)e * FR + pix * 3) * 4 + 3 * k + ch] =
-                                k == 3 ? px[ch] : ring[((size_t)s * S.N + e) * FR + pix * 3 + ch];
-                    }
-                } else {
-                    for (int ch = 0; ch < 3; ch++) o1[(size_t)e * FR + pix * 3 + ch] = px[ch];
-                    bool stacked = (pp == MG_PREPROC_LORES4E && view == 1) || (pp == MG_PREPROC_LORES4A && view == 0);
-                    if (stacked) {
-                        for (int k = 0; k < 4; k++) {
-                            int s = (nh + 1 + k) & 3;
-                            for (int ch = 0; ch < 3; ch++)
-                                out.obs_past[((size_t)e * FR + pix * 3) * 4 + 3 * k + ch] =
-                                    k == 3 ? px[ch] : ring[((size_t)s * S.N + e) * FR + pix * 3 + ch];
-                        }
-                    }
-                }
+                uint4 w;
+                w.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+                w.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
+                w.z = b[8] | (b[9] << 8) | (b[10] << 16) | ((uint32_t)b[11] << 24);
+                w.w = b[12] | (b[13] << 8) | (b[14] << 16) | ((uint32_t)b[15] << 24);
+                *(uint4 *)(o_stack + (size_t)e * FR * 4 + lrow * 4 + 16 * c) = w;
             }
         }
         __syncthreads();

@@ -175,9 +175,10 @@ static void layout(MGState &S, Carver &c) {
 static hipStream_t as_stream(void *s) { return (hipStream_t)s; }
 static int grid64(const mg_sim *s) { return (s->S.n_envs + 63) / 64; }
 
-static int render_lores(mg_sim *s, hipStream_t st) {
+static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
     RenderOut ro;
     ro.full = nullptr;
+    ro.mask = mask;
     ro.obs_allo = s->out.obs_allo; ro.obs_ego = s->out.obs_ego; ro.obs_past = s->out.obs_past;
     ro.preproc = s->preproc;
     hipLaunchKernelGGL(render_kernel, dim3(s->S.n_envs, 2), dim3(RG_THREADS), 0, st, s->S, s->dlib, ro, 0);
@@ -244,6 +245,9 @@ int mg_bind_outputs(mg_sim *s, const mg_buffers *b) {
         return set_err(-22, "mg_bind_outputs: obs_allo / obs_ego required");
     if ((s->preproc == MG_PREPROC_LORES4E || s->preproc == MG_PREPROC_LORES4A) && !b->obs_past)
         return set_err(-22, "mg_bind_outputs: obs_past required for this preprocessor");
+    const void *ptrs[3] = {b->obs_allo, b->obs_ego, b->obs_past};
+    for (const void *p : ptrs)
+        if (((uintptr_t)p & 15) != 0) return set_err(-22, "mg_bind_outputs: observation buffers must be 16-byte aligned");
     s->out = *b;
     s->bound = 1;
     return 0;
@@ -257,7 +261,7 @@ int mg_reset(mg_sim *s, const uint8_t *mask, void *stream) {
     TaskCfg cfg = {s->task, s->flags};
     hipLaunchKernelGGL(reset_kernel, dim3(grid64(s)), dim3(64), 0, st, s->S, s->dlib, cfg, mask);
     HIPC(hipGetLastError());
-    if (s->preproc != MG_PREPROC_NONE) return render_lores(s, st);
+    if (s->preproc != MG_PREPROC_NONE) return render_lores(s, st, mask);
     return 0;
 }
 
@@ -275,7 +279,7 @@ int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
     HIPC(hipGetLastError());
     if (ev) HIPC(hipEventRecord(ev[1], st));
     int rc = 0;
-    if (s->preproc != MG_PREPROC_NONE) rc = render_lores(s, st);
+    if (s->preproc != MG_PREPROC_NONE) rc = render_lores(s, st, nullptr);
     if (ev) HIPC(hipEventRecord(ev[2], st));
     return rc;
 }

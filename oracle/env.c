@@ -81,6 +81,7 @@ static void render_both(OEnv *e, uint8_t *allo384, uint8_t *ego384) {
 }
 
 int oenv_reset(OEnv *e, uint8_t *obs) {
+    e->placement_error = 0;
     oscene_reset(e);
     uint8_t *a = (uint8_t *)malloc((size_t)O_RES * O_RES * 3), *g = (uint8_t *)malloc((size_t)O_RES * O_RES * 3);
     render_both(e, a, g);
@@ -91,6 +92,7 @@ int oenv_reset(OEnv *e, uint8_t *obs) {
     if (obs) write_obs(e, obs, a, g);
     free(a); free(g);
     e->last_score = 0.0;
+    if (e->placement_error) return -2;
     return e->space.overflow ? -1 : 0;
 }
 

@@ -87,6 +87,8 @@ void oenv_destroy(OEnv *e);
 void oenv_seed(OEnv *e, uint32_t seed);
 /* bytes of one observation for this preproc (all keys concatenated in dict order) */
 int oenv_obs_bytes(const OEnv *e);
+/* 0 ok; -1 table overflow; -2 PlacementError (geom.py:335-336 raises; the
+ * reference env would crash, the state is left as after the last retry) */
 int oenv_reset(OEnv *e, uint8_t *obs);
 int oenv_step(OEnv *e, int action, uint8_t *obs, double *reward, int *done, double *eval_score);
 /* full-resolution views of the current state: [384][384][3] each */

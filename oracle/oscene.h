@@ -50,6 +50,7 @@ struct OEnv {
     double pv[5]; /* PhysicsVariables: robot_pos, robot_rot, finger, shape_trans, shape_rot */
     double target_speed, rel_turn, target_finger;
     int episode_steps;
+    int placement_error; /* geom.py:335-336: PlacementError after max_retries */
     double last_score;
     /* LoRes frame history (newest last) */
     uint8_t hist_allo[4][O_LORES * O_LORES * 3];

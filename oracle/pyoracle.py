@@ -103,6 +103,10 @@ def star_parts(out_rad, in_rad):
     return parts
 
 
+class PlacementError(RuntimeError):
+    pass
+
+
 class OracleEnv:
     """One reference env (single instance, CPU)."""
 
@@ -124,6 +128,8 @@ class OracleEnv:
     def reset(self):
         obs = np.zeros(self.nbytes, dtype=np.uint8)
         rc = self.L.oenv_reset(self.h, ptr(obs))
+        if rc == -2:
+            raise PlacementError("could not place entities after 10 retries (geom.py:335-336)")
         if rc != 0:
             raise RuntimeError("oracle table overflow")
         return obs

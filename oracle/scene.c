@@ -678,6 +678,7 @@ static void randomise_all_poses(OEnv *e, const int *ents, int n, const int *rand
         }
         if (!failed) return;
     }
+    e->placement_error = 1;
 }
 
 /* geom.py:344-359 */
