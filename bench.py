@@ -65,7 +65,8 @@ def load_pmc(kernel):
         return None
     with open(path) as f:
         data = json.load(f)
-    return data.get(kernel)
+    rec = data.get(kernel)
+    return rec["bytes_per_launch"] if rec else None
 
 
 def main():

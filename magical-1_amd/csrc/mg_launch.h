@@ -1,0 +1,25 @@
+// mg_launch.h -- host-side launchers of the device kernels (one translation unit
+// per kernel family: mg_physics.hip, mg_raster.hip; the C ABI lives in mg_sim.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "mg_state.h"
+
+struct TaskCfg { int task, flags; };
+
+struct RenderOut {
+    uint8_t *full;        // [N][2][384][384][3] (full-resolution mode) or null
+    uint8_t *obs_allo;    // LoRes outputs (layout per preproc), or null
+    uint8_t *obs_ego;
+    uint8_t *obs_past;
+    const uint8_t *mask;  // reset mask: envs with mask[e] == 0 are left untouched (null: all)
+    int preproc;
+};
+
+hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream_t st);
+hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, const uint8_t *mask, hipStream_t st);
+hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, int max_steps, int auto_reset,
+                          const uint8_t *actions, float *reward, uint8_t *done, double *eval_score, hipStream_t st);
+hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderOut &ro, int mode, hipStream_t st);
+// profiling builds (-DMG_PROFILE): copy and clear each translation unit's phase timers
+hipError_t mg_prof_read_physics(unsigned long long *out64);
+hipError_t mg_prof_read_raster(unsigned long long *out64);

@@ -3,50 +3,67 @@
 // Replaces render.py:151-287 / 385-395 (Geom.render, Poly._render ->
 // pygame.draw.polygon + width-2 lines + dashed width-4 goal outlines,
 // surfarray) and benchmarks/__init__.py:150-190 (cv2.resize INTER_AREA 4x).
-// The 384x384 frame never leaves the CU: it is produced in 8-row bands in LDS
-// where each covered pixel receives atomicMax(draw ordinal) -- the painter's
-// algorithm is "the last primitive drawn wins", i.e. the maximum ordinal -- so
-// every fill span and outline pixel can be rasterised concurrently.  Each
-// finished band is reduced 4x4 -> 2 output rows (round half to even of
-// sum/16, OpenCV resizeAreaFast) and written straight to HBM.
+//
+// The 384x384 frame never leaves the CU.  Setup (per workgroup) turns the
+// scene into integer vertices, per-row fill spans (pygame draw_fillpoly) and a
+// per-band list of outline segments.  The frame is then produced in 8-row bands:
+// outline pixels go to an LDS layer by atomicMax(draw ordinal) -- the painter's
+// rule "last primitive drawn wins" is "largest ordinal wins" -- and one thread
+// per 4x4 block resolves fills (geoms in draw order), takes the max with the
+// outline layer, looks up colours and sums the block (cv2 INTER_AREA 4x:
+// round-half-even of sum/16).  Each band yields 2 LoRes rows written to HBM
+// with 16-byte stores, together with the frame-stack ring.
 #pragma once
+#include "mg_launch.h"
 #include "mg_step.h"
+#include "mg_prof.h"
 
 #define RG_MAXG 160
 #define RG_MAXVERT 2048
 #define RG_MAXSPAN 6144
-#define RG_MAXDASH 512
+#define RG_MAXDASH 384
+#define RG_MAXBIN 2048
+#define RG_MAXLONG 64
 #define RG_BAND 8
-#define RG_THREADS 256
+#define RG_NBANDS (MG_RES / RG_BAND)
+#define RG_THREADS 192                  // = one thread per 4x4 block of a band (2 x 96)
+#define RG_SHORT 16                     // segments with <= RG_SHORT pixels in a band: drawn by their own thread
+#define RG_SPAN_SHORT 24                // fill edges spanning <= RG_SPAN_SHORT rows: one thread
+#define RG_EMPTY 32767
 #define RG_LOROW (MG_LORES * 3)         // bytes of one 96-px RGB row
 #define RG_BANDLO (2 * RG_LOROW)        // bytes of the 2 LoRes rows one band produces
 #define RG_BANDLO16 (RG_BANDLO / 16)    // ... in 16-byte chunks (36)
 
-struct RenderOut {
-    uint8_t *full;      // [N][2][384][384][3] (full-resolution mode) or null
-    uint8_t *obs_allo;  // LoRes outputs (layout per preproc), or null
-    uint8_t *obs_ego;
-    uint8_t *obs_past;
-    const uint8_t *mask;  // reset mask: envs with mask[e] == 0 are left untouched (null: all)
-    int preproc;
-};
 
-// LDS: the setup stages (matrices) and the band stages (band buffer + LoRes
-// staging) never live at the same time, so they share storage.
+// A pygame drawline pixel run in k-form: the major axis has n = max(|dx|,|dy|) + 1
+// pixels and the minor offset of pixel k is m = floor(k * dminor / dmajor) with
+// DX = |dx| + 1, DY = |dy| + 1 (horizontal and vertical lines are the cases
+// DY = 1 / DX = 1).  x-major (DX >= DY): pixel (x1 + sgx*k, y1 + sgy*m);
+// y-major: (x1 + sgx*m, y1 + sgy*k).
+struct LineK { int x1, y1, sgx, sgy, DX, DY, xmaj; };
+
+// LDS: the setup matrices, the span bookkeeping and the band buffers are never
+// live at the same time, so they share storage.
 struct RenderSmem {
-    union {
+    union alignas(16) {
         struct {
             double g_m[RG_MAXG][6];
             double e_xf[MG_MAX_ENTS][5][9];
             double view[9];
         } pre;
         struct {
-            uint32_t band[RG_BAND][MG_RES];
+            uint32_t scnt[RG_MAXSPAN / 4];  // per span row: #side-A (low nibble) / #side-B (high) intersections
+            int16_t lspan[256];             // fill edges spanning many rows (processed cooperatively)
+        } mid;
+        struct {
+            uint32_t band[RG_BAND][MG_RES]; // outline layer of the current band
             uint4 lo[RG_BANDLO16];          // current frame, 2 LoRes rows
             uint4 past[3][RG_BANDLO16];     // frames t-3, t-2, t-1 of the same rows
+            int32_t lk[RG_MAXLONG][7];      // long segments of this band (LineK)
+            int32_t lkr[RG_MAXLONG][3];     // klo, khi, ordinal
         } post;
     } u;
-    int16_t g_rpoly[RG_MAXG], g_voff[RG_MAXG], g_nv[RG_MAXG];
+    int16_t g_rpoly[RG_MAXG], g_voff[RG_MAXG + 1], g_nv[RG_MAXG];
     int16_t g_ymin[RG_MAXG], g_ymax[RG_MAXG], g_xmin[RG_MAXG], g_xmax[RG_MAXG];
     int8_t g_ent[RG_MAXG];
     int32_t g_soff[RG_MAXG + 1];
@@ -54,17 +71,47 @@ struct RenderSmem {
     int16_t vx[RG_MAXVERT], vy[RG_MAXVERT];   // int pixel vertices (fill, line ends)
     int16_t fx[RG_MAXVERT], fy[RG_MAXVERT];   // float->int first points of solid outline edges
     uint8_t v_geom[RG_MAXVERT];
-    int16_t sedge[RG_MAXVERT];                // solid outline edges (start vertex)
-    int16_t span_l[RG_MAXSPAN], span_r[RG_MAXSPAN];
+    uint16_t sedge[RG_MAXVERT];               // solid outline edges: start vertex | last << 14 | inside << 15
+    int16_t span[RG_MAXSPAN][2];              // fill intersections of the two y-monotone chains
+    uint4 ginfo[RG_MAXG];                     // (ymin|ymax<<16, xmin|xmax<<16, span base, fill ordinal)
+    int16_t blist[RG_MAXG];                   // geoms overlapping the current band, in draw order
     int16_t dash[RG_MAXDASH][4];              // clipped dashed-outline lines
     int16_t dash_o[RG_MAXDASH];
-    uint32_t col[2 * RG_MAXG + 2];
-    int32_t ngeom, nvert, nspan, nsedge, ndash, err;
+    int16_t bin_off[RG_NBANDS + 1];           // per-band outline item lists
+    int32_t bin_cnt[RG_NBANDS];
+    int16_t bin[RG_MAXBIN];
+    uint64_t col[2 * RG_MAXG + 2];            // R | G << 16 | B << 32 per ordinal
+    int32_t ngeom, nvert, nspan, nsedge, ndash, nlspan, nlong, nblist, err;
+#ifdef MG_PROFILE
+    unsigned int pw[4];
+#endif
 };
 
-MG_DEV uint32_t pack_rgb(const uint8_t *c) { return (uint32_t)c[0] | ((uint32_t)c[1] << 8) | ((uint32_t)c[2] << 16); }
+// Workgroup barrier ordering LDS only (s_waitcnt lgkmcnt(0); s_barrier): unlike
+// __syncthreads it does not wait for outstanding global loads/stores, so the
+// frame-stack prefetch and the output stores stay in flight across bands.  No
+// thread of a workgroup reads global memory another thread of it wrote.
+#define RG_SYNC() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
-MG_DEV uint32_t ref_colour(const mg_library *L, int ref, int ecol) {
+// exclusive prefix sum over in[0, n) (n <= 256) into out[0, n]; out[n] = total.
+// Called by the 64 lanes of wave 0; in and out may alias.
+template <typename TI, typename TO>
+MG_DEV void wave_exclusive_scan(const TI *in, TO *out, int n, int lane) {
+    int v[4], s = 0;
+    for (int k = 0; k < 4; k++) { int i = 4 * lane + k; v[k] = i < n ? (int)in[i] : 0; s += v[k]; }
+    int incl = s;
+    for (int off = 1; off < 64; off <<= 1) {
+        int t = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += t;
+    }
+    int ex = incl - s;
+    for (int k = 0; k < 4; k++) { int i = 4 * lane + k; if (i < n) out[i] = (TO)ex; ex += v[k]; }
+    if (lane == 63) out[n] = (TO)incl;
+}
+
+MG_DEV uint64_t pack_rgb(const uint8_t *c) { return (uint64_t)c[0] | ((uint64_t)c[1] << 16) | ((uint64_t)c[2] << 32); }
+
+MG_DEV uint64_t ref_colour(const mg_library *L, int ref, int ecol) {
     switch (ref) {
     case MG_RC_ENT_BASE: return pack_rgb(L->palette[ecol][0]);
     case MG_RC_ENT_DARK: return pack_rgb(L->palette[ecol][1]);
@@ -170,49 +217,87 @@ MG_DEV void band_put(RenderSmem &sm, int x, int y, int y0, uint32_t ord) {
     if (r >= 0 && r < RG_BAND && x >= 0 && x < MG_RES) atomicMax(&sm.u.post.band[r][x], ord);
 }
 
-// all pixels of a clipped line (pygame drawline) within rows [y0, y0 + RG_BAND)
-MG_DEV void raster_line_band(RenderSmem &sm, int x1, int y1, int x2, int y2, uint32_t ord, int y0) {
-    int y1b = y0 + RG_BAND - 1;
-    if (y1 == y2) {
-        if (y1 < y0 || y1 > y1b) return;
-        int xa = x1 < x2 ? x1 : x2, xb = x1 < x2 ? x2 : x1;
-        for (int x = xa; x <= xb; x++) band_put(sm, x, y1, y0, ord);
-        return;
+// pygame drawline of a clipped segment in k-form (major axis has |d|+1 pixels,
+// minor offset of pixel k = floor(k * dminor / dmajor))
+MG_DEV LineK line_k(int x1, int y1, int x2, int y2) {
+    const int dx = x2 - x1, dy = y2 - y1;
+    const int sgx = dx < 0 ? -1 : 1, sgy = dy < 0 ? -1 : 1;
+    const int DX = sgx * dx + 1, DY = sgy * dy + 1;
+    return {x1, y1, sgx, sgy, DX, DY, DX >= DY ? 1 : 0};
+}
+
+// the k-range [klo, khi] of a segment's pixels inside rows [y0, y0 + RG_BAND)
+MG_DEV void band_krange(const LineK &L, int y0, int &klo, int &khi) {
+    // row index along the segment (m for x-major, k for y-major) in [0, DY)
+    int mlo = L.sgy > 0 ? y0 - L.y1 : L.y1 - (y0 + RG_BAND - 1);
+    int mhi = mlo + RG_BAND - 1;
+    mlo = mlo > 0 ? mlo : 0;
+    mhi = mhi < L.DY - 1 ? mhi : L.DY - 1;
+    if (L.xmaj) {
+        const int kl = (mlo * L.DX + L.DY - 1) / L.DY;            // smallest k with k*DY >= mlo*DX
+        const int kh = ((mhi + 1) * L.DX + L.DY - 1) / L.DY - 1;  // largest k with k*DY < (mhi+1)*DX
+        klo = kl; khi = kh < L.DX - 1 ? kh : L.DX - 1;
+    } else {
+        klo = mlo; khi = mhi;
     }
-    if (x1 == x2) {
-        int ya = y1 < y2 ? y1 : y2, yb = y1 < y2 ? y2 : y1;
-        ya = ya > y0 ? ya : y0; yb = yb < y1b ? yb : y1b;
-        for (int y = ya; y <= yb; y++) band_put(sm, x1, y, y0, ord);
-        return;
-    }
-    // drawline: major axis has (|d|+1) pixels; minor offset of pixel k = floor(k * dminor / dmajor)
-    int dx = x2 - x1, dy = y2 - y1;
-    int sgx = dx < 0 ? -1 : 1, sgy = dy < 0 ? -1 : 1;
-    int DX = sgx * dx + 1, DY = sgy * dy + 1;
-    if (DX >= DY) { // x major
-        // rows y1 + sgy*m, m = floor(k*DY/DX); keep m with row in band
-        int mlo, mhi;
-        if (sgy > 0) { mlo = y0 - y1; mhi = y1b - y1; } else { mlo = y1 - y1b; mhi = y1 - y0; }
-        if (mlo < 0) mlo = 0;
-        if (mhi > DY - 1) mhi = DY - 1;
-        if (mlo > mhi) return;
-        int klo = (mlo * DX + DY - 1) / DY;            // smallest k with k*DY >= mlo*DX
-        int khi = ((mhi + 1) * DX + DY - 1) / DY - 1;  // largest k with k*DY < (mhi+1)*DX
-        if (khi > DX - 1) khi = DX - 1;
-        for (int k = klo; k <= khi; k++) band_put(sm, x1 + sgx * k, y1 + sgy * ((k * DY) / DX), y0, ord);
-    } else { // y major: pixel k at row y1 + sgy*k
-        int klo, khi;
-        if (sgy > 0) { klo = y0 - y1; khi = y1b - y1; } else { klo = y1 - y1b; khi = y1 - y0; }
-        if (klo < 0) klo = 0;
-        if (khi > DY - 1) khi = DY - 1;
-        for (int k = klo; k <= khi; k++) band_put(sm, x1 + sgx * ((k * DX) / DY), y1 + sgy * k, y0, ord);
+    if (mlo > mhi) { klo = 0; khi = -1; }
+}
+
+// pixels k in [ka, kb] of a segment; the minor offset is stepped incrementally
+MG_DEV void raster_krange(RenderSmem &sm, const LineK &L, int ka, int kb, int y0, uint32_t ord) {
+    const int dmaj = L.xmaj ? L.DX : L.DY, dmin = L.xmaj ? L.DY : L.DX;
+    const int ax = L.xmaj ? L.sgx : 0, ay = L.xmaj ? 0 : L.sgy;   // per k
+    const int bx = L.xmaj ? 0 : L.sgx, by = L.xmaj ? L.sgy : 0;   // per m
+    int m = (ka * dmin) / dmaj, acc = ka * dmin - m * dmaj;
+    for (int k = ka; k <= kb; k++) {
+        band_put(sm, L.x1 + ax * k + bx * m, L.y1 + ay * k + by * m, y0, ord);
+        acc += dmin;
+        if (acc >= dmaj) { acc -= dmaj; m++; }
     }
 }
 
-// one sub-line of a width-2 outline: clip (pygame clipline) then raster in band
-MG_DEV void clip_raster_band(RenderSmem &sm, int x1, int y1, int x2, int y2, uint32_t ord, int y0) {
-    if (!clipline(x1, y1, x2, y2)) return;
-    raster_line_band(sm, x1, y1, x2, y2, ord, y0);
+// one clipped segment: short runs are drawn here, long runs are queued for the whole workgroup
+MG_DEV void segment_band(RenderSmem &sm, int x1, int y1, int x2, int y2, uint32_t ord, int y0) {
+    int klo, khi;
+    const LineK L = line_k(x1, y1, x2, y2);
+    band_krange(L, y0, klo, khi);
+    if (khi < klo) return;
+    if (khi - klo + 1 > RG_SHORT) {
+        int q = atomicAdd(&sm.nlong, 1);
+        if (q < RG_MAXLONG) {
+            int32_t *d = sm.u.post.lk[q];
+            d[0] = L.x1; d[1] = L.y1; d[2] = L.sgx; d[3] = L.sgy; d[4] = L.DX; d[5] = L.DY; d[6] = L.xmaj;
+            sm.u.post.lkr[q][0] = klo; sm.u.post.lkr[q][1] = khi; sm.u.post.lkr[q][2] = (int32_t)ord;
+            return;
+        }
+    }
+    raster_krange(sm, L, klo, khi, y0, ord);
+}
+
+// end points of solid outline edge k: (float->int first point) -> (int next vertex)
+MG_DEV void edge_ends(const RenderSmem &sm, int k, int &x1, int &y1, int &x2, int &y2, uint32_t &ord, bool &inside) {
+    const uint32_t se = sm.sedge[k];
+    const int v = se & 0x3FFF, g = sm.v_geom[v];
+    const int nx = (se & 0x4000u) ? v + 1 - sm.g_nv[g] : v + 1;
+    x1 = sm.fx[v]; y1 = sm.fy[v]; x2 = sm.vx[nx]; y2 = sm.vy[nx];
+    ord = 2 * g + 2;
+    inside = (se & 0x8000u) != 0;
+}
+
+// rows covered by outline item i (solid edge sub-lines or a dash line), before clipping
+MG_DEV void item_rows(const RenderSmem &sm, int i, int &ylo, int &yhi) {
+    if (i < sm.nsedge) {
+        int x1, y1, x2, y2;
+        uint32_t ord;
+        bool inside;
+        edge_ends(sm, i, x1, y1, x2, y2, ord, inside);
+        ylo = y1 < y2 ? y1 : y2;
+        yhi = (y1 > y2 ? y1 : y2) + 1;  // the width-2 copy may sit one row lower
+    } else {
+        const int16_t *d = sm.dash[i - sm.nsedge];
+        ylo = d[1] < d[3] ? d[1] : d[3];
+        yhi = d[1] > d[3] ? d[1] : d[3];
+    }
 }
 
 // render polygon point i (local coordinates); the goal rect is make_rect(w, h) of its entity
@@ -246,8 +331,9 @@ MG_DEV void entity_xforms(const MGState &S, int e, int ent, double (*xf)[9]) {
 __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out,
                                                             int mode) {
     __shared__ RenderSmem sm;
-    const int e = blockIdx.x, view = blockIdx.y, tid = threadIdx.x;
+    const int e = blockIdx.x, view = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
     if (e >= S.n_envs || (out.mask && !out.mask[e])) return;
+    MG_PROF_BEGIN(tid == 0);
     const int nents = S.nents[e];
     // ---- 1. geometry list (entity add order x render polys), colour table, view ----
     int my_r0 = 0, my_nr = 0;
@@ -260,10 +346,11 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         sm.e_g0[tid + 1] = (int16_t)my_nr;
     }
     if (tid == 0) {
-        sm.err = 0; sm.ndash = 0; sm.nsedge = 0;
+        sm.err = 0; sm.ndash = 0; sm.nsedge = 0; sm.nlspan = 0; sm.nlong = 0;
         sm.col[0] = pack_rgb(L->background);
         sm.e_g0[0] = 0;
     }
+    if (tid < RG_NBANDS) sm.bin_cnt[tid] = 0;
     if (view == 0 && tid == 32) { // Viewer.render: stack.push(self.transform) -> eye(3) @ view
         const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
         mg_mat3_mul(I3, L->allo_view, sm.u.pre.view);
@@ -282,13 +369,13 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         mg_mat3_mul(I3, m1, sm.u.pre.view);
     }
     if (tid >= 64 && tid - 64 < nents) entity_xforms(S, e, tid - 64, sm.u.pre.e_xf[tid - 64]);
-    __syncthreads();
+    RG_SYNC();
     if (tid == 0) {
         for (int k = 0; k < nents; k++) sm.e_g0[k + 1] += sm.e_g0[k];
         sm.ngeom = sm.e_g0[nents];
         if (sm.ngeom > RG_MAXG) sm.err = 2;
     }
-    __syncthreads();
+    RG_SYNC();
     if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
     const int G = sm.ngeom;
     if (tid < nents) {
@@ -299,16 +386,11 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             sm.g_ent[g] = (int8_t)tid;
             sm.g_nv[g] = (int16_t)rp.npts;
             sm.col[2 * g + 1] = ref_colour(L, rp.col_ref, ecol);
-            sm.col[2 * g + 2] = rp.outline ? ref_colour(L, rp.ocol_ref, ecol) : 0u;
+            sm.col[2 * g + 2] = rp.outline ? ref_colour(L, rp.ocol_ref, ecol) : 0ull;
         }
     }
-    __syncthreads();
-    if (tid == 0) {
-        int nv = 0;
-        for (int g = 0; g < G; g++) { sm.g_voff[g] = (int16_t)nv; nv += sm.g_nv[g]; }
-        sm.nvert = nv;
-        if (nv > RG_MAXVERT) sm.err = 2;
-    }
+    RG_SYNC();
+    if (tid < 64) wave_exclusive_scan(sm.g_nv, sm.g_voff, G, lane);
     // ---- 2. per-geom matrix: view @ T_last @ ... @ T_first (Geom.render stack) ----
     for (int g = tid; g < G; g += RG_THREADS) {
         const mg_rpoly &rp = L->rpoly[sm.g_rpoly[g]];
@@ -322,12 +404,12 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         }
         for (int i = 0; i < 6; i++) sm.u.pre.g_m[g][i] = M[i];
     }
-    __syncthreads();
-    if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
-    const int NV = sm.nvert;
+    RG_SYNC();
+    const int NV = sm.g_voff[G];
+    if (NV > RG_MAXVERT) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
     for (int g = tid; g < G; g += RG_THREADS)
         for (int i = 0, v0 = sm.g_voff[g]; i < sm.g_nv[g]; i++) sm.v_geom[v0 + i] = (uint8_t)g;
-    __syncthreads();
+    RG_SYNC();
     // ---- 3. vertices -> int pixel coordinates (pygame (int) truncation); outline edges ----
     for (int v = tid; v < NV; v += RG_THREADS) {
         int g = sm.v_geom[v], i = v - sm.g_voff[g];
@@ -343,7 +425,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             // lines(): first point via float (pg FloatFromObj), second via int
             sm.fx[v] = (int16_t)(int)(float)gx;
             sm.fy[v] = (int16_t)(int)(float)gy;
-            sm.sedge[atomicAdd(&sm.nsedge, 1)] = (int16_t)v;
+            sm.sedge[atomicAdd(&sm.nsedge, 1)] = (uint16_t)(v | (i + 1 == rp.npts ? 0x4000 : 0));
         } else if (rp.outline == MG_OUTLINE_DASHED) {
             int j = i + 1 == rp.npts ? 0 : i + 1;
             double xb, yb;
@@ -352,8 +434,8 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             push_dashes(sm, gx, gy, gxb, gyb, 2 * g + 2);
         }
     }
-    __syncthreads();
-    // ---- 4. per-geom bounding rows / columns; span table offsets ----
+    RG_SYNC();
+    // ---- 4. per-geom bounding rows / columns; span rows; outline items per band ----
     for (int g = tid; g < G; g += RG_THREADS) {
         int v0 = sm.g_voff[g], n = sm.g_nv[g];
         int ymin = sm.vy[v0], ymax = ymin, xmin = sm.vx[v0], xmax = xmin;
@@ -366,49 +448,102 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         sm.g_xmin[g] = (int16_t)(xmin > 0 ? xmin : 0);
         sm.g_xmax[g] = (int16_t)(xmax < MG_RES - 1 ? xmax : MG_RES - 1);
         int r0 = ymin > 0 ? ymin : 0, r1 = ymax < MG_RES - 1 ? ymax : MG_RES - 1;
-        sm.g_soff[g + 1] = r1 >= r0 ? r1 - r0 + 1 : 0;
+        sm.g_soff[g] = r1 >= r0 ? r1 - r0 + 1 : 0;
     }
-    __syncthreads();
-    if (tid == 0) {
-        sm.g_soff[0] = 0;
-        for (int g = 0; g < G; g++) sm.g_soff[g + 1] += sm.g_soff[g];
-        sm.nspan = sm.g_soff[G];
-        if (sm.nspan > RG_MAXSPAN) sm.err = 3;
-    }
-    __syncthreads();
-    if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
-    // ---- 5. fill spans: pygame draw_fillpoly intersections per row (2 per row for these convex polys) ----
-    for (int s = tid; s < sm.nspan; s += RG_THREADS) {
-        int lo_g = 0, hi_g = G - 1; // last g with g_soff[g] <= s
-        while (lo_g < hi_g) {
-            int mid = (lo_g + hi_g + 1) >> 1;
-            if (sm.g_soff[mid] <= s) lo_g = mid; else hi_g = mid - 1;
+    if (sm.ndash > RG_MAXDASH) sm.err = 1;
+    const int nitems = sm.nsedge + (sm.ndash < RG_MAXDASH ? sm.ndash : RG_MAXDASH);
+    for (int i = tid; i < nitems; i += RG_THREADS) {
+        int ylo, yhi;
+        item_rows(sm, i, ylo, yhi);
+        if (i < sm.nsedge) { // both width-2 sub-lines inside the surface: clipping is the identity
+            int x1, y1, x2, y2;
+            uint32_t ord;
+            bool inside;
+            edge_ends(sm, i, x1, y1, x2, y2, ord, inside);
+            int xl = x1 < x2 ? x1 : x2, xh = x1 > x2 ? x1 : x2;
+            if (xl >= 0 && xh + 1 <= MG_RES - 1 && ylo >= 0 && yhi <= MG_RES - 1) sm.sedge[i] |= 0x8000u;
         }
-        const int g = lo_g;
-        int ymin = sm.g_ymin[g], ymax = sm.g_ymax[g];
-        int y = (ymin > 0 ? ymin : 0) + s - sm.g_soff[g];
-        int v0 = sm.g_voff[g], n = sm.g_nv[g];
-        int lo = 32767, hi = -32768, cnt = 0;
-        for (int i = 0; i < n; i++) {
-            int ip = i ? i - 1 : n - 1;
-            int ya = sm.vy[v0 + ip], yb = sm.vy[v0 + i], xa, xb;
-            if (ya < yb) { xa = sm.vx[v0 + ip]; xb = sm.vx[v0 + i]; }
-            else if (ya > yb) { int t = ya; ya = yb; yb = t; xa = sm.vx[v0 + i]; xb = sm.vx[v0 + ip]; }
-            else continue;
-            if ((y >= ya && y < yb) || (y == ymax && y > ya && y <= yb)) {
-                int x = (y - ya) * (xb - xa) / (yb - ya) + xa;
-                lo = x < lo ? x : lo; hi = x > hi ? x : hi;
-                cnt++;
-            }
-        }
-        if (cnt != 0 && cnt != 2) sm.err = 4;
-        if (cnt == 0) { lo = 32767; hi = -32768; }
-        sm.span_l[s] = (int16_t)lo;
-        sm.span_r[s] = (int16_t)hi;
+        ylo = ylo > 0 ? ylo : 0; yhi = yhi < MG_RES - 1 ? yhi : MG_RES - 1;
+        for (int b = ylo / RG_BAND; b <= yhi / RG_BAND && ylo <= yhi; b++) atomicAdd(&sm.bin_cnt[b], 1);
     }
-    __syncthreads();
+    RG_SYNC();
+    if (tid < 64) {
+        wave_exclusive_scan(sm.g_soff, sm.g_soff, G, lane);
+        wave_exclusive_scan(sm.bin_cnt, sm.bin_off, RG_NBANDS, lane);
+    }
+    RG_SYNC();
+    const int nspan = sm.g_soff[G];
+    if (nspan > RG_MAXSPAN || sm.bin_off[RG_NBANDS] > RG_MAXBIN) sm.err = 3;
+    if (tid < RG_NBANDS) sm.bin_cnt[tid] = sm.bin_off[tid];
+    for (int g = tid; g < G; g += RG_THREADS) {
+        const int ymin = sm.g_ymin[g];
+        sm.ginfo[g] = make_uint4((uint32_t)(uint16_t)ymin | ((uint32_t)(uint16_t)sm.g_ymax[g] << 16),
+                                 (uint32_t)(uint16_t)sm.g_xmin[g] | ((uint32_t)(uint16_t)sm.g_xmax[g] << 16),
+                                 (uint32_t)(sm.g_soff[g] - (ymin > 0 ? ymin : 0)), (uint32_t)(2 * g + 1));
+    }
+    for (int s = tid; s < nspan; s += RG_THREADS) { sm.span[s][0] = RG_EMPTY; sm.span[s][1] = RG_EMPTY; }
+    for (int s = tid; s < RG_MAXSPAN / 4; s += RG_THREADS) sm.u.mid.scnt[s] = 0u;
+    RG_SYNC();
     if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
-    const int ndash = sm.ndash, nsedge = sm.nsedge;
+    for (int i = tid; i < nitems; i += RG_THREADS) {
+        int ylo, yhi;
+        item_rows(sm, i, ylo, yhi);
+        ylo = ylo > 0 ? ylo : 0; yhi = yhi < MG_RES - 1 ? yhi : MG_RES - 1;
+        for (int b = ylo / RG_BAND; b <= yhi / RG_BAND && ylo <= yhi; b++)
+            sm.bin[atomicAdd(&sm.bin_cnt[b], 1)] = (int16_t)i;
+    }
+    // ---- 5. fill spans (pygame draw_fillpoly): an edge from vertex i-1 to i with ya < yb meets rows
+    //         ya <= y < yb, plus y == yb when yb is the polygon's max row.  The two y-monotone chains of
+    //         these convex polygons (edges going down / up) give the two intersections of every row. ----
+    for (int v = tid; v < NV; v += RG_THREADS) {
+        const int g = sm.v_geom[v], v0 = sm.g_voff[g], n = sm.g_nv[g];
+        const int ip = v == v0 ? v0 + n - 1 : v - 1;
+        const int ya = sm.vy[ip], yb = sm.vy[v];
+        if (ya == yb) continue;
+        const int ymax = sm.g_ymax[g];
+        const int lo = ya < yb ? ya : yb, hi = ya < yb ? yb : ya;
+        const int r0 = sm.g_ymin[g] > 0 ? sm.g_ymin[g] : 0, r1 = ymax < MG_RES - 1 ? ymax : MG_RES - 1;
+        const int ys = lo > r0 ? lo : r0, ye = (hi == ymax ? hi : hi - 1) < r1 ? (hi == ymax ? hi : hi - 1) : r1;
+        if (ye - ys + 1 > RG_SPAN_SHORT) { int q = atomicAdd(&sm.nlspan, 1); if (q < 256) sm.u.mid.lspan[q] = (int16_t)v; continue; }
+        const int xa = ya < yb ? sm.vx[ip] : sm.vx[v], xb = ya < yb ? sm.vx[v] : sm.vx[ip];
+        const int side = ya < yb ? 0 : 1;
+        const uint32_t inc = ya < yb ? 1u : 16u;
+        const int sb = sm.g_soff[g] - r0;
+        for (int y = ys; y <= ye; y++) {
+            sm.span[sb + y][side] = (int16_t)((y - lo) * (xb - xa) / (hi - lo) + xa);
+            atomicAdd(&sm.u.mid.scnt[(sb + y) >> 2], inc << (8 * ((sb + y) & 3)));
+        }
+    }
+    RG_SYNC();
+    const int nls = sm.nlspan < 256 ? sm.nlspan : 256;
+    if (sm.nlspan > 256) sm.err = 3;
+    for (int q = 0; q < nls; q++) {
+        const int v = sm.u.mid.lspan[q];
+        const int g = sm.v_geom[v], v0 = sm.g_voff[g], n = sm.g_nv[g];
+        const int ip = v == v0 ? v0 + n - 1 : v - 1;
+        const int ya = sm.vy[ip], yb = sm.vy[v], ymax = sm.g_ymax[g];
+        const int lo = ya < yb ? ya : yb, hi = ya < yb ? yb : ya;
+        const int r0 = sm.g_ymin[g] > 0 ? sm.g_ymin[g] : 0, r1 = ymax < MG_RES - 1 ? ymax : MG_RES - 1;
+        const int ys = lo > r0 ? lo : r0, ye = (hi == ymax ? hi : hi - 1) < r1 ? (hi == ymax ? hi : hi - 1) : r1;
+        const int xa = ya < yb ? sm.vx[ip] : sm.vx[v], xb = ya < yb ? sm.vx[v] : sm.vx[ip];
+        const int side = ya < yb ? 0 : 1;
+        const uint32_t inc = ya < yb ? 1u : 16u;
+        const int sb = sm.g_soff[g] - r0;
+        for (int y = ys + tid; y <= ye; y += RG_THREADS) {
+            sm.span[sb + y][side] = (int16_t)((y - lo) * (xb - xa) / (hi - lo) + xa);
+            atomicAdd(&sm.u.mid.scnt[(sb + y) >> 2], inc << (8 * ((sb + y) & 3)));
+        }
+    }
+    RG_SYNC();
+    // every row: no intersection, or exactly one per chain (else the fill assumption is violated)
+    for (int s = tid; s < nspan; s += RG_THREADS) {
+        uint32_t c = (sm.u.mid.scnt[s >> 2] >> (8 * (s & 3))) & 255u;
+        if (c != 0u && c != 17u) sm.err = 4;
+    }
+    RG_SYNC();
+    if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
+    const int nsedge = sm.nsedge;
+    MG_PROF(0);
     // ---- 6. bands ----
     uint8_t *ring = view == 0 ? S.hist_allo : S.hist_ego;
     const size_t FR = (size_t)MG_LORES * MG_LORES * 3;
@@ -421,7 +556,8 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     const bool plain = pp != MG_PREPROC_LORESSTACK;   // the view's own current-frame output
     uint8_t *o_plain = view == 0 ? out.obs_allo : out.obs_ego;
     uint8_t *o_stack = pp == MG_PREPROC_LORESSTACK ? o_plain : out.obs_past;
-    for (int y0 = 0; y0 < MG_RES; y0 += RG_BAND) {
+    const int oyl = tid / MG_LORES, ox = tid % MG_LORES, x0 = 4 * ox;
+    for (int y0 = 0, band_i = 0; y0 < MG_RES; y0 += RG_BAND, band_i++) {
         const size_t lrow = (size_t)(y0 / 4) * RG_LOROW;  // byte offset of this band's LoRes rows
         // prefetch frames t-3..t-1 of these rows (ring slots nh+1..nh+3, never written this step)
         uint4 pf = make_uint4(0, 0, 0, 0);
@@ -430,65 +566,133 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             int k = tid / RG_BANDLO16, c = tid % RG_BANDLO16, sl = (nh + 1 + k) & 3;
             pf = *(const uint4 *)(ring + ((size_t)sl * S.N + e) * FR + lrow + 16 * c);
         }
-        for (int i = tid; i < RG_BAND * MG_RES; i += RG_THREADS) (&sm.u.post.band[0][0])[i] = 0u;
-        __syncthreads();
-        for (int g = 0; g < G; g++) {
-            int ymin = sm.g_ymin[g], ymax = sm.g_ymax[g];
-            int ra = ymin > y0 ? ymin : y0, rb = ymax < y0 + RG_BAND - 1 ? ymax : y0 + RG_BAND - 1;
-            if (ra > rb) continue;
-            int xmin = sm.g_xmin[g], xmax = sm.g_xmax[g];
-            if (xmin > xmax) continue;
-            int w = xmax - xmin + 1, total = (rb - ra + 1) * w;
-            int r0 = ymin > 0 ? ymin : 0;
-            uint32_t ord = 2 * g + 1;
-            for (int i = tid; i < total; i += RG_THREADS) {
-                int y = ra + i / w, x = xmin + i % w;
-                int s = sm.g_soff[g] + y - r0;
-                if (x >= sm.span_l[s] && x <= sm.span_r[s]) atomicMax(&sm.u.post.band[y - y0][x], ord);
-            }
-        }
-        // solid width-2 outlines (clip_and_draw_line_width: base line + one offset copy)
-        for (int k = tid; k < nsedge; k += RG_THREADS) {
-            int v = sm.sedge[k], g = sm.v_geom[v];
-            int nx = v + 1 == sm.g_voff[g] + sm.g_nv[g] ? sm.g_voff[g] : v + 1;
-            int x1 = sm.fx[v], y1 = sm.fy[v], x2 = sm.vx[nx], y2 = sm.vy[nx];
-            int ylo = (y1 < y2 ? y1 : y2) - 1, yhi = (y1 > y2 ? y1 : y2) + 1;
-            if (yhi < y0 || ylo >= y0 + RG_BAND) continue;
-            uint32_t ord = 2 * g + 2;
-            clip_raster_band(sm, x1, y1, x2, y2, ord, y0);
-            if (abs(x1 - x2) > abs(y1 - y2)) clip_raster_band(sm, x1, y1 + 1, x2, y2 + 1, ord, y0);
-            else clip_raster_band(sm, x1 + 1, y1, x2 + 1, y2, ord, y0);
-        }
-        for (int i = tid; i < ndash; i += RG_THREADS)
-            raster_line_band(sm, sm.dash[i][0], sm.dash[i][1], sm.dash[i][2], sm.dash[i][3], (uint32_t)sm.dash_o[i], y0);
-        __syncthreads();
-        if (mode == 1) {
-            uint8_t *dst = out.full + (((size_t)e * 2 + view) * MG_RES + y0) * MG_RES * 3;
-            for (int i = tid; i < RG_BAND * MG_RES; i += RG_THREADS) {
-                uint32_t c = sm.col[(&sm.u.post.band[0][0])[i]];
-                dst[3 * i] = (uint8_t)(c & 255); dst[3 * i + 1] = (uint8_t)((c >> 8) & 255); dst[3 * i + 2] = (uint8_t)(c >> 16);
-            }
-            __syncthreads();
-            continue;
-        }
-        // 4x4 area downsample (round half to even of sum/16) into LDS staging
-        uint8_t *lo8 = (uint8_t *)sm.u.post.lo;
-        for (int t = tid; t < (RG_BAND / 4) * MG_LORES; t += RG_THREADS) {
-            int oyl = t / MG_LORES, ox = t % MG_LORES;
-            int sr = 0, sg = 0, sb = 0;
-            for (int dy = 0; dy < 4; dy++)
-                for (int dx = 0; dx < 4; dx++) {
-                    uint32_t c = sm.col[sm.u.post.band[oyl * 4 + dy][ox * 4 + dx]];
-                    sr += c & 255; sg += (c >> 8) & 255; sb += c >> 16;
+        // outline layer: ordinals of outline pixels (atomicMax), 0 elsewhere
+        for (int i = tid; i < RG_BAND * MG_RES / 4; i += RG_THREADS)
+            ((uint4 *)&sm.u.post.band[0][0])[i] = make_uint4(0, 0, 0, 0);
+        if (tid == 0) sm.nlong = 0;
+        if (tid < 64) { // geoms whose rows meet this band, in draw order (ballot compaction)
+            int cnt = 0;
+            for (int base = 0; base < G; base += 64) {
+                const int g = base + lane;
+                bool ov = false;
+                if (g < G) {
+                    const uint4 gi = sm.ginfo[g];
+                    const int ymin = (int16_t)(gi.x & 0xFFFF), ymax = (int16_t)(gi.x >> 16);
+                    const int xmin = (int16_t)(gi.y & 0xFFFF), xmax = (int16_t)(gi.y >> 16);
+                    ov = ymax >= y0 && ymin < y0 + RG_BAND && xmin <= xmax;
                 }
-            int ss[3] = {sr, sg, sb};
-            for (int ch = 0; ch < 3; ch++) {
-                int q = ss[ch] >> 4, r = ss[ch] & 15;
-                lo8[t * 3 + ch] = (uint8_t)(q + (r > 8 || (r == 8 && (q & 1))));
+                const uint64_t m = __ballot(ov);
+                if (ov) sm.blist[cnt + __popcll(m & ((1ull << lane) - 1ull))] = (int16_t)g;
+                cnt += __popcll(m);
+            }
+            if (lane == 0) sm.nblist = cnt;
+        }
+        RG_SYNC();
+        MG_PROF(1);
+#ifdef MG_PROFILE
+        if (tid < 4) sm.pw[tid] = 0u;
+#endif
+        MG_PROF_MARK(t_lines);
+        // outline items of this band: solid width-2 edges (clip_and_draw_line_width: base line plus one
+        // offset copy, each clipped) and clipped dashed-goal lines
+        for (int j = sm.bin_off[band_i] + tid; j < sm.bin_off[band_i + 1]; j += RG_THREADS) {
+            const int i = sm.bin[j];
+            if (i < nsedge) {
+                int x1, y1, x2, y2;
+                uint32_t ord;
+                bool inside;
+                edge_ends(sm, i, x1, y1, x2, y2, ord, inside);
+                const bool xmaj = abs(x1 - x2) > abs(y1 - y2);
+#pragma unroll 1
+                for (int c = 0; c < 2; c++) {
+                    int a1 = x1 + (c && !xmaj), b1 = y1 + (c && xmaj), a2 = x2 + (c && !xmaj), b2 = y2 + (c && xmaj);
+                    if (inside || clipline(a1, b1, a2, b2)) segment_band(sm, a1, b1, a2, b2, ord, y0);
+                }
+            } else {
+                const int16_t *d = sm.dash[i - nsedge];
+                segment_band(sm, d[0], d[1], d[2], d[3], (uint32_t)sm.dash_o[i - nsedge], y0);
             }
         }
+        MG_PROF_MAXW(sm.pw[0], t_lines);
+        RG_SYNC();
+        const int nlong = sm.nlong;
+        if (nlong > 0) {
+            for (int q = 0; q < nlong; q++) {
+                const int32_t *d = q < RG_MAXLONG ? sm.u.post.lk[q] : nullptr;
+                if (!d) break;
+                LineK Lk = {d[0], d[1], d[2], d[3], d[4], d[5], d[6]};
+                const uint32_t ord = (uint32_t)sm.u.post.lkr[q][2];
+                const int klo = sm.u.post.lkr[q][0], khi = sm.u.post.lkr[q][1];
+                const int chunk = (khi - klo + RG_THREADS) / RG_THREADS;  // ceil(n / threads)
+                const int ka = klo + tid * chunk, kb = ka + chunk - 1 < khi ? ka + chunk - 1 : khi;
+                if (ka <= kb) raster_krange(sm, Lk, ka, kb, y0, ord);
+            }
+            RG_SYNC();
+        }
+        MG_PROF(2);
+        // fill + resolve, one thread per 4x4 block: painter's order over geoms (later fill
+        // wins), max with the outline layer, colour, then the area sum of the block
+        uint8_t *lo8 = (uint8_t *)sm.u.post.lo;
+        MG_PROF_MARK(t_fill);
+        {
+            const int yb = y0 + 4 * oyl;
+            uint32_t o[4][4];
+            for (int r = 0; r < 4; r++)
+                for (int c = 0; c < 4; c++) o[r][c] = 0u;
+            const int nbl = sm.nblist;
+            for (int i = 0; i < nbl; i++) {
+                const uint4 gi = sm.ginfo[sm.blist[i]];
+                const int ymin = (int16_t)(gi.x & 0xFFFF), ymax = (int16_t)(gi.x >> 16);
+                const int xmin = (int16_t)(gi.y & 0xFFFF), xmax = (int16_t)(gi.y >> 16);
+                if (ymax < yb || ymin > yb + 3 || xmax < x0 || xmin > x0 + 3) continue;
+                const int sbase = (int)gi.z;
+                const uint32_t ord = gi.w;
+                uint32_t sp[4];
+                for (int r = 0; r < 4; r++)
+                    sp[r] = (yb + r >= ymin && yb + r <= ymax) ? *(const uint32_t *)&sm.span[sbase + yb + r][0] : 0u;
+                for (int r = 0; r < 4; r++) {
+                    const int y = yb + r;
+                    if (y < ymin || y > ymax) continue;
+                    const int sa = (int16_t)(sp[r] & 0xFFFF), sb = (int16_t)(sp[r] >> 16);
+                    const int l = sa < sb ? sa : sb, rr = sa < sb ? sb : sa;
+                    for (int c = 0; c < 4; c++)
+                        if (x0 + c >= l && x0 + c <= rr) o[r][c] = ord;
+                }
+            }
+            uint64_t sum = 0;
+            for (int r = 0; r < 4; r++) {
+                const uint4 lv = *(const uint4 *)&sm.u.post.band[4 * oyl + r][x0];
+                o[r][0] = o[r][0] > lv.x ? o[r][0] : lv.x;
+                o[r][1] = o[r][1] > lv.y ? o[r][1] : lv.y;
+                o[r][2] = o[r][2] > lv.z ? o[r][2] : lv.z;
+                o[r][3] = o[r][3] > lv.w ? o[r][3] : lv.w;
+                for (int c = 0; c < 4; c++) sum += sm.col[o[r][c]];
+            }
+            if (mode == 1) {
+                for (int r = 0; r < 4; r++) {
+                    uint8_t *dst = out.full + ((((size_t)e * 2 + view) * MG_RES + yb + r) * MG_RES + x0) * 3;
+                    for (int c = 0; c < 4; c++) {
+                        const uint64_t cc = sm.col[o[r][c]];
+                        dst[3 * c] = (uint8_t)cc; dst[3 * c + 1] = (uint8_t)(cc >> 16); dst[3 * c + 2] = (uint8_t)(cc >> 32);
+                    }
+                }
+            } else {
+                for (int ch = 0; ch < 3; ch++) {
+                    const int ss = (int)((sum >> (16 * ch)) & 0xFFFF);
+                    const int q = ss >> 4, rm = ss & 15;
+                    lo8[tid * 3 + ch] = (uint8_t)(q + (rm > 8 || (rm == 8 && (q & 1))));
+                }
+            }
+        }
+        MG_PROF_MAXW(sm.pw[1], t_fill);
+        if (mode == 1) { RG_SYNC(); continue; }
         if (do_pf) sm.u.post.past[tid / RG_BANDLO16][tid % RG_BANDLO16] = pf;
-        __syncthreads();
+        RG_SYNC();
+        MG_PROF(3);
+#ifdef MG_PROFILE
+        _pacc[5] += sm.pw[0]; _pacc[6] += sm.pw[1]; _pacc[7] += nlong; _pacc[8] += sm.bin_off[band_i + 1] - sm.bin_off[band_i];
+        _pacc[9] += sm.nblist;
+#endif
         // ring of the last 4 LoRes frames: slot nh (all 4 slots at episode start)
         for (int t = tid; t < (fresh ? 4 : 1) * RG_BANDLO16; t += RG_THREADS) {
             int sl = fresh ? t / RG_BANDLO16 : nh, c = t % RG_BANDLO16;
@@ -515,7 +719,9 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
                 *(uint4 *)(o_stack + (size_t)e * FR * 4 + lrow * 4 + 16 * c) = w;
             }
         }
-        __syncthreads();
+        RG_SYNC();
+        MG_PROF(4);
     }
     if (mode == 0 && tid == 0) S.hist_head[view * S.N + e] = nh;
+    MG_PROF_END(16 * view);
 }

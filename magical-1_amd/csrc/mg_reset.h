@@ -8,6 +8,7 @@
 // match_regions.py:44-191.  RNG: numpy legacy RandomState (MT19937) per env,
 // drawn in the reference's order so parity mode replays the reference stream.
 #pragma once
+#include "mg_launch.h"
 #include "mg_step.h"
 
 #define MT(i) S.mt_key[(size_t)(i) * (size_t)S.N + (size_t)e]
@@ -291,7 +292,6 @@ MG_DEV void randomise_all(const MGState &S, const mg_library *L, int e, const in
 }
 
 // ---- tasks -----------------------------------------------------------------
-struct TaskCfg { int task, flags; };
 __constant__ static const int MG_SHAPE_COLOURS[4] = {MG_COL_RED, MG_COL_GREEN, MG_COL_BLUE, MG_COL_YELLOW};
 __constant__ static const int MG_SHAPE_TYPES[4] = {MG_SHAPE_SQUARE, MG_SHAPE_PENTAGON, MG_SHAPE_STAR, MG_SHAPE_CIRCLE};
 

@@ -1,9 +1,10 @@
 // mg_sim.hip -- gfx950 kernels and the C ABI (include/magical_sim.h).
 //
-// Per env-step (mg_step): step_kernel (one env per lane: action decode,
-// 10 x [Robot.update + cpSpaceStep], episode counter, score, in-place reset
-// of finished episodes) then render_kernel (one workgroup per (env, view):
-// 384^2 raster in LDS bands -> 96^2 area downsample -> LoRes frame stack).
+// Per env-step (mg_step): step_kernel (mg_physics.hip: one env per lane: action
+// decode, 10 x [Robot.update + cpSpaceStep], episode counter, score, in-place
+// reset of finished episodes) then render_kernel (mg_raster.hip: one workgroup
+// per (env, view): 384^2 raster in LDS bands -> 96^2 area downsample -> LoRes
+// frame stack).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstring>
@@ -12,8 +13,8 @@
 #include <vector>
 
 #include "../../include/magical_sim.h"
-#include "mg_render.h"
-#include "mg_score.h"
+#include "mg_launch.h"
+#include "mg_phys.h"
 
 static thread_local std::string g_err;
 static int set_err(int code, const std::string &msg) {
@@ -42,42 +43,6 @@ struct mg_sim {
 
 // ---------------------------------------------------------------------------
 // kernels
-__global__ void __launch_bounds__(64) seed_kernel(MGState S, const uint32_t *__restrict__ seeds) {
-    int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= S.n_envs) return;
-    mt_seed(S, e, seeds[e]);
-}
-
-__global__ void __launch_bounds__(64) reset_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg,
-                                                   const uint8_t *__restrict__ mask) {
-    int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= S.n_envs) return;
-    if (mask && !mask[e]) return;
-    reset_env(S, L, e, cfg);
-}
-
-__global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg, int max_steps,
-                                                  int auto_reset, const uint8_t *__restrict__ actions, float *reward,
-                                                  uint8_t *done, double *eval_score) {
-    int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= S.n_envs) return;
-    int a = actions[e];
-    robot_set_action(S, L, e, a < 18 ? a : 0);
-    const double dt = L->dt;
-    for (int i = 0; i < 10; i++) {
-        robot_update(S, L, e);
-        space_step(S, L, e, dt);
-    }
-    int steps = S.episode_steps[e] + 1;
-    S.episode_steps[e] = steps;
-    bool d = max_steps > 0 && steps >= max_steps;
-    double sc = d ? score_env(S, L, e, cfg.task) : 0.0;
-    if (reward) reward[e] = (float)sc;
-    if (done) done[e] = d ? 1 : 0;
-    if (eval_score) eval_score[e] = sc;
-    if (d && auto_reset) reset_env(S, L, e, cfg); // VecEnv auto-reset: next obs is the new episode's first frame
-}
-
 __global__ void __launch_bounds__(64) bodies_kernel(MGState S, double *out, int32_t *counts) {
     int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= S.n_envs) return;
@@ -181,8 +146,7 @@ static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
     ro.mask = mask;
     ro.obs_allo = s->out.obs_allo; ro.obs_ego = s->out.obs_ego; ro.obs_past = s->out.obs_past;
     ro.preproc = s->preproc;
-    hipLaunchKernelGGL(render_kernel, dim3(s->S.n_envs, 2), dim3(RG_THREADS), 0, st, s->S, s->dlib, ro, 0);
-    HIPC(hipGetLastError());
+    HIPC(mg_launch_render(s->S, s->dlib, ro, 0, st));
     return 0;
 }
 
@@ -191,6 +155,17 @@ static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
 extern "C" {
 
 const char *mg_last_error(void) { return g_err.c_str(); }
+
+#ifdef MG_PROFILE
+// profiling builds only (tools/gpu_phase.py): phase timer totals, then cleared
+int mg_debug_read_profile(unsigned long long *out) {
+    HIPC(hipDeviceSynchronize());
+    for (int i = 0; i < 64; i++) out[i] = 0;
+    HIPC(mg_prof_read_physics(out));
+    HIPC(mg_prof_read_raster(out));
+    return 0;
+}
+#endif
 
 int mg_create(const mg_config *cfg, mg_sim **out) {
     if (!cfg || !out) return set_err(-22, "mg_create: null argument");
@@ -232,8 +207,7 @@ int mg_seed(mg_sim *s, const uint32_t *seeds_host) {
     uint32_t *d = nullptr;
     HIPC(hipMalloc(&d, sizeof(uint32_t) * s->S.n_envs));
     HIPC(hipMemcpy(d, seeds_host, sizeof(uint32_t) * s->S.n_envs, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(seed_kernel, dim3(grid64(s)), dim3(64), 0, 0, s->S, d);
-    HIPC(hipGetLastError());
+    HIPC(mg_launch_seed(s->S, d, 0));
     HIPC(hipDeviceSynchronize());
     HIPC(hipFree(d));
     return 0;
@@ -259,8 +233,7 @@ int mg_reset(mg_sim *s, const uint8_t *mask, void *stream) {
     HIPC(hipSetDevice(s->device));
     hipStream_t st = as_stream(stream);
     TaskCfg cfg = {s->task, s->flags};
-    hipLaunchKernelGGL(reset_kernel, dim3(grid64(s)), dim3(64), 0, st, s->S, s->dlib, cfg, mask);
-    HIPC(hipGetLastError());
+    HIPC(mg_launch_reset(s->S, s->dlib, cfg, mask, st));
     if (s->preproc != MG_PREPROC_NONE) return render_lores(s, st, mask);
     return 0;
 }
@@ -274,9 +247,8 @@ int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
     hipEvent_t *ev = nullptr;
     if (s->timing && s->ev_used + 3 <= s->ev.size()) { ev = &s->ev[s->ev_used]; s->ev_used += 3; }
     if (ev) HIPC(hipEventRecord(ev[0], st));
-    hipLaunchKernelGGL(step_kernel, dim3(grid64(s)), dim3(64), 0, st, s->S, s->dlib, cfg, s->max_steps, s->auto_reset, actions,
-                       s->out.reward, s->out.done, s->out.eval_score);
-    HIPC(hipGetLastError());
+    HIPC(mg_launch_step(s->S, s->dlib, cfg, s->max_steps, s->auto_reset, actions, s->out.reward, s->out.done,
+                        s->out.eval_score, st));
     if (ev) HIPC(hipEventRecord(ev[1], st));
     int rc = 0;
     if (s->preproc != MG_PREPROC_NONE) rc = render_lores(s, st, nullptr);
@@ -291,8 +263,7 @@ int mg_render_full(mg_sim *s, uint8_t *out, void *stream) {
     memset(&ro, 0, sizeof(ro));
     ro.full = out;
     ro.preproc = s->preproc;
-    hipLaunchKernelGGL(render_kernel, dim3(s->S.n_envs, 2), dim3(RG_THREADS), 0, as_stream(stream), s->S, s->dlib, ro, 1);
-    HIPC(hipGetLastError());
+    HIPC(mg_launch_render(s->S, s->dlib, ro, 1, as_stream(stream)));
     return 0;
 }
 

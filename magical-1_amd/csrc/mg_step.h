@@ -4,6 +4,7 @@
 // (Robot.set_action / Robot.update), base_env.py:248-255 (10 substeps).
 #pragma once
 #include "mg_phys.h"
+#include "mg_prof.h"
 
 // ---- body access with the static body as zeros --------------------------
 struct BodyR { int b; double minv, iinv; };
@@ -310,7 +311,7 @@ MG_DEV void arbiter_apply(const MGState &S, int e, int slot) {
 }
 
 // ---- cpSpaceStep -----------------------------------------------------------
-MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt) {
+MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, MGProf &P) {
     uint32_t stamp = S.stamp[e] + 1;
     S.stamp[e] = stamp;
     double prev_dt = S.curr_dt[e];
@@ -327,6 +328,7 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt) 
     }
     int ns = S.nshapes[e];
     for (int k = 0; k < ns; k++) shape_update_bb(S, L, e, k);
+    MG_PP(P, 1);
     // broadphase + narrowphase, canonical order
     for (int i = 0; i < ns; i++) {
         ShapeW A;
@@ -354,6 +356,7 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt) 
             if (info.count) arbiter_update(S, L, e, i * 128 + j, A, B, ui, AT(S.su, j), info);
         }
     }
+    MG_PP(P, 2);
     // cached arbiter filter
     for (int i = 0; i < MG_MAX_ARB; i++) {
         if (AT(S.akey, i) < 0) continue;
@@ -361,18 +364,22 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt) 
         if (ticks >= 1 && AT(S.astate, i) != ARB_CACHED) AT(S.astate, i) = ARB_CACHED;
         if (ticks >= 3) { AT(S.akey, i) = -1; AT(S.acount, i) = 0; }
     }
+    MG_PP(P, 3);
     nact = S.nactive[e];
     int nc = S.ncons[e];
     for (int i = 0; i < nact; i++) arbiter_prestep(S, L, e, AT(S.active, i), dt);
     for (int c = 0; c < nc; c++) cons_prestep(S, e, c, dt);
+    MG_PP(P, 4);
     // velocity integration is the identity here (no gravity, damping 1, no forces)
     double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
     for (int i = 0; i < nact; i++) arbiter_cached(S, e, AT(S.active, i), dt_coef);
     for (int c = 0; c < nc; c++) cons_cached(S, e, c, dt_coef);
+    MG_PP(P, 5);
     for (int it = 0; it < 10; it++) {
         for (int i = 0; i < nact; i++) arbiter_apply(S, e, AT(S.active, i));
         for (int c = 0; c < nc; c++) cons_apply(S, e, c, dt);
     }
+    MG_PP(P, 6);
 }
 
 // ---- robot control ---------------------------------------------------------

@@ -1,7 +1,10 @@
-"""Build the in-tree HIP library: python -m magical_amd.build
+"""Build the in-tree HIP library: python -m magical_amd.build [--force] [--profile]
 
-hipcc --offload-arch=gfx950 with -ffp-contract=off (no fused multiply-add
-except the explicit __fma_rn that reproduces numpy's BLAS arithmetic).
+Three translation units compiled in parallel for gfx950 (hipcc
+--offload-arch=gfx950, -ffp-contract=off: no fused multiply-add except the
+explicit __fma_rn that reproduces numpy's BLAS arithmetic), then linked into
+magical_amd/libmagical_sim.so.  Objects are rebuilt only when their sources
+change.  --profile builds libmagical_sim_prof.so with -DMG_PROFILE phase timers.
 """
 import os
 import subprocess
@@ -9,32 +12,52 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+INCLUDE = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "magical_sim.h")
+OBJDIR = os.path.join(os.path.dirname(HERE), "build")
 OUT = os.path.join(HERE, "libmagical_sim.so")
-SOURCES = ["mg_sim.hip"]
-HEADERS = ["mg_common.h", "mg_math.h", "mg_state.h", "mg_phys.h", "mg_step.h", "mg_reset.h", "mg_score.h",
-           "mg_render.h"]
+PROF_OUT = os.path.join(HERE, "libmagical_sim_prof.so")  # -DMG_PROFILE phase timers (tools/gpu_phase.py)
+_COMMON = ["mg_common.h", "mg_math.h", "mg_state.h", "mg_launch.h", "mg_prof.h"]
+_PHYS = _COMMON + ["mg_phys.h", "mg_step.h"]
+UNITS = {  # translation unit -> headers it depends on
+    "mg_sim.hip": _COMMON + ["mg_phys.h"],
+    "mg_physics.hip": _PHYS + ["mg_reset.h", "mg_score.h"],
+    "mg_raster.hip": _PHYS + ["mg_render.h"],
+}
+FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-Wno-unused-result"]
 
 
-def _stale():
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps.append(os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "magical_sim.h"))
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+def _mtime(p):
+    return os.path.getmtime(p) if os.path.exists(p) else 0.0
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
-        return OUT
-    cmd = ["hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-shared",
-           "-Wno-unused-result", "-o", OUT + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True, cwd=CSRC)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+def build(force=False, verbose=False, profile=False):
+    out = PROF_OUT if profile else OUT
+    tag = "prof" if profile else "opt"
+    os.makedirs(OBJDIR, exist_ok=True)
+    procs, objs = [], []
+    for unit, headers in UNITS.items():
+        obj = os.path.join(OBJDIR, unit.replace(".hip", f".{tag}.o"))
+        objs.append(obj)
+        deps = [os.path.join(CSRC, unit), INCLUDE] + [os.path.join(CSRC, h) for h in headers]
+        if not force and _mtime(obj) > max(_mtime(d) for d in deps):
+            continue
+        cmd = ["hipcc"] + FLAGS + (["-DMG_PROFILE"] if profile else []) + ["-c", os.path.join(CSRC, unit),
+                                                                         "-o", obj + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append((subprocess.Popen(cmd, cwd=CSRC), obj))
+    for p, obj in procs:
+        if p.wait() != 0:
+            raise RuntimeError(f"hipcc failed for {obj}")
+        os.replace(obj + ".tmp", obj)
+    if force or procs or _mtime(out) < max(_mtime(o) for o in objs):
+        cmd = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, profile="--profile" in sys.argv))

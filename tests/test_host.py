@@ -1,0 +1,190 @@
+"""CPU: host-side logic -- env-name registry, C-ABI library exports, the
+observation layout helpers and the multi-process sharding path (gloo)."""
+import ctypes
+import os
+import re
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import magical_amd
+from magical_amd import dist as mdist
+from magical_amd import native, registry
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+# --------------------------------------------------------------------------- registry
+def test_registry_matches_golden_table():
+    import json
+    g = json.load(open(os.path.join(GOLDEN, "registry.json")))
+    assert list(registry.ALL_REGISTERED_ENVS) == g["names"]
+    assert len(g["names"]) == 441
+    for lit in g["reference_literals"]:
+        if lit != "-v0":
+            assert lit in registry.SPECS, lit
+
+
+def test_env_name_grammar_and_update():
+    n = registry.EnvName("MoveToCorner-TestAll-LoResStack-v0")
+    assert (n.task, n.variant, n.preproc, n.version, n.is_test) == ("MoveToCorner", "TestAll", "LoResStack", "v0", True)
+    assert n.demo_env_name == "MoveToCorner-Demo-LoResStack-v0"
+    assert registry.update_magical_env_name("MoveToCorner-Demo-v0", preproc="LoRes4E") == "MoveToCorner-Demo-LoRes4E-v0"
+    assert registry.update_magical_env_name("MoveToCorner-Demo-LoRes4E-v0", variant="TestJitter") == \
+        "MoveToCorner-TestJitter-LoRes4E-v0"
+    with pytest.raises(ValueError):
+        registry.EnvName("not-an-env")
+
+
+def test_specs_of_bench_configs():
+    s = registry.lookup("MoveToRegion-Demo-LoRes4E-v0")
+    assert (s.task, s.rand_flags, s.preproc, s.max_episode_steps) == ("MoveToRegion", 0, "LoRes4E", 40)
+    s = registry.lookup("MatchRegions-TestAll-LoRes4E-v0")
+    assert s.rand_flags == 2 | 4 | 8 | 16 | 32 and s.max_episode_steps == 120
+    s = registry.lookup("ClusterColour-Demo-LoResStack-v0")
+    assert s.max_episode_steps == 240 and s.preproc == "LoResStack"
+    assert registry.lookup("MoveToCorner-Demo-DebugReward-LoRes4E-v0").preproc is None  # fork quirk
+    assert registry.PREPROCESSORS["LoResCHW4A"] == registry.PREPROCESSORS["LoResCHW4E"]
+    with pytest.raises(KeyError):
+        registry.lookup("MoveToRegion-Demo-LoRes9X-v0")
+
+
+def test_demo_to_test_map():
+    m = registry.DEMO_ENVS_TO_TEST_ENVS_MAP
+    assert "MoveToRegion-Demo-v0" in m
+    assert "MoveToRegion-TestAll-v0" in m["MoveToRegion-Demo-v0"]
+    assert all(registry.EnvName(t).is_test for ts in m.values() for t in ts)
+
+
+def test_observation_spaces():
+    from magical_amd.envs import _obs_shapes
+    assert dict(_obs_shapes(registry.lookup("MoveToRegion-Demo-LoRes4E-v0"))) == \
+        {"allo": (96, 96, 3), "ego": (96, 96, 3), "past_obs": (96, 96, 12)}
+    assert dict(_obs_shapes(registry.lookup("MoveToRegion-Demo-LoResCHW4E-v0")))["past_obs"] == (12, 96, 96)
+    shapes = _obs_shapes(registry.lookup("ClusterColour-Demo-LoResStack-v0"))
+    assert sum(int(np.prod(s)) for s in shapes.values()) == 2 * 96 * 96 * 12
+
+
+# --------------------------------------------------------------------------- C ABI
+def _header_functions():
+    src = open(os.path.join(ROOT, "include", "magical_sim.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mg_[a-z_]+)\s*\(", src)))
+
+
+def test_header_and_binding_agree():
+    assert _header_functions() == sorted(native.EXPORTS)
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    lib = native.load()
+    for name in _header_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", native.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (mg_\w+)", out))
+    assert set(_header_functions()) <= exported
+
+
+def test_library_is_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list", "--type=o",
+                          f"--input={native.LIB_PATH}"], capture_output=True, text=True)
+    if out.returncode != 0:
+        data = open(native.LIB_PATH, "rb").read()
+        assert b"gfx950" in data
+    else:
+        assert "gfx950" in out.stdout
+
+
+def test_abi_argument_validation_without_gpu():
+    lib = native.load()
+    h = ctypes.c_void_p()
+    assert lib.mg_create(None, ctypes.byref(h)) != 0
+    assert b"null" in lib.mg_last_error()
+    cfg = native.mg_config(task=0, rand_flags=0, preproc=1, num_envs=4, device=0, max_episode_steps=40,
+                           base_seed=0, auto_reset=1, seeds=None, library=None, library_size=3)
+    assert lib.mg_create(ctypes.byref(cfg), ctypes.byref(h)) != 0
+    assert b"library_size" in lib.mg_last_error()
+    assert lib.mg_step(None, None, None) != 0
+    assert lib.mg_read_timing(None, None) != 0
+
+
+def test_product_path_has_no_cpu_fallback(tmp_path, monkeypatch):
+    monkeypatch.setattr(native, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(native, "_lib", None)
+    with pytest.raises(native.NativeError):
+        native.load()
+
+
+# --------------------------------------------------------------------------- sharding
+def test_shard_seeds_partition_the_global_batch():
+    w, n = 4, 5
+    allseeds = sum((mdist.shard_seeds(n, r) for r in range(w)), [])
+    assert allseeds == [1000 + i for i in range(w * n)]
+    assert mdist.shard_range(n, 2) == (10, 15)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+WORKER = r'''
+import os, sys
+sys.path[:0] = [{root!r} + "/magical-1_amd", {root!r} + "/oracle"]
+import numpy as np, torch, torch.distributed as dist
+import pyoracle as po
+from magical_amd import dist as mdist, registry
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", init_method="env://")
+spec = registry.lookup("MoveToRegion-Demo-LoRes4E-v0")
+n, steps = 2, 6
+envs = [po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, spec.max_episode_steps, seed=s)
+        for s in mdist.shard_seeds(n, rank)]
+obs = np.stack([e.reset() for e in envs])
+acts = np.random.RandomState(5).randint(0, 18, (steps, world * n))
+lo, hi = mdist.shard_range(n, rank)
+for t in range(steps):
+    obs = np.stack([e.step(int(a))[0] for e, a in zip(envs, acts[t, lo:hi])])
+full = mdist.all_gather_batch({{"obs": torch.from_numpy(obs)}})["obs"].numpy()
+el = torch.tensor([float(rank + 1)], dtype=torch.float64)
+dist.all_reduce(el, op=dist.ReduceOp.MAX)
+if rank == 0:
+    np.save({out!r}, full)
+    assert el.item() == world
+dist.destroy_process_group()
+'''
+
+
+def test_two_rank_gloo_sharded_rollout_equals_single_process(tmp_path):
+    """world_size 2 on CPU: each rank runs its contiguous shard, the gathered
+    batch equals one process running all envs (seed/order bookkeeping of the
+    multi-GPU path), and max-over-ranks timing reduction works."""
+    out = str(tmp_path / "full.npy")
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER.format(root=ROOT, out=out))
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env))
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    full = np.load(out)
+    import pyoracle as po
+    spec = registry.lookup("MoveToRegion-Demo-LoRes4E-v0")
+    acts = np.random.RandomState(5).randint(0, 18, (6, 4))
+    envs = [po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, spec.max_episode_steps, seed=1000 + i)
+            for i in range(4)]
+    for e in envs:
+        e.reset()
+    for t in range(6):
+        ref = np.stack([e.step(int(a))[0] for e, a in zip(envs, acts[t])])
+    assert np.array_equal(full, ref)

@@ -1,0 +1,56 @@
+"""Phase breakdown of the step and render kernels (profiling build).
+
+MAGICAL_AMD_PROFILE=1 python tools/gpu_phase.py [env] [envs] [steps]
+Loads libmagical_sim_prof.so (-DMG_PROFILE): one lane per wave (physics) /
+thread 0 per workgroup (render) accumulates s_memtime deltas per phase.
+Render phases are measured after each barrier, so a phase includes the wait
+for the slowest wave of the workgroup.
+"""
+import ctypes
+import os
+import sys
+
+os.environ["MAGICAL_AMD_PROFILE"] = "1"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "magical-1_amd")]
+import torch  # noqa: E402
+import magical_amd  # noqa: E402
+from magical_amd import native  # noqa: E402
+
+name = sys.argv[1] if len(sys.argv) > 1 else "MoveToRegion-Demo-LoRes4E-v0"
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+vec = magical_amd.make_vec(name, n, seeds=[1000 + i for i in range(n)])
+lib = native.load()
+lib.mg_debug_read_profile.argtypes = [ctypes.c_void_p]
+buf = (ctypes.c_ulonglong * 64)()
+acts = torch.empty(n, dtype=torch.uint8, device="cuda")
+vec.reset()
+for s in range(5):
+    vec.random_actions(s, out=acts)
+    vec.step(acts)
+torch.cuda.synchronize()
+lib.mg_debug_read_profile(buf)
+for s in range(steps):
+    vec.random_actions(100 + s, out=acts)
+    vec.step(acts)
+torch.cuda.synchronize()
+lib.mg_debug_read_profile(buf)
+v = list(buf)
+R = ["setup(1-5)", "band clear+prefetch", "band lines", "band fill+resolve", "band output"]
+X = ["max-thread lines work", "max-thread fill work", "long segments", "bin items", "band geoms"]
+P = ["robot_update", "integrate+bb", "broad+narrow", "arb filter", "prestep", "cached impulses", "iterations",
+     "tail(score/reset)"]
+for view, base in (("allo", 0), ("ego", 16)):
+    tot = sum(v[base:base + 5])
+    print(f"render {view}: total {tot / 1e6:.1f}M ticks over {steps} steps x {n} WGs")
+    for i, nm in enumerate(R):
+        print(f"   {nm:22s} {v[base + i] / max(tot, 1) * 100:6.1f}%  {v[base + i] / (steps * n):10.0f} ticks/WG")
+    for i, nm in enumerate(X):
+        print(f"   {nm:22s} {v[base + 5 + i] / (steps * n):10.1f} per WG (sum over bands)")
+tot = sum(v[32:40])
+waves = (n + 63) // 64
+print(f"physics: total {tot / 1e6:.1f}M ticks, {waves} waves")
+for i, nm in enumerate(P):
+    print(f"   {nm:22s} {v[32 + i] / max(tot, 1) * 100:6.1f}%  {v[32 + i] / (steps * waves):10.0f} ticks/wave-step")
+vec.close()

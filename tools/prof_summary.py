@@ -1,0 +1,76 @@
+"""Summarise rocprofv3 rocpd databases (kernel-trace stats and PMC passes).
+
+python tools/prof_summary.py gpurun_out/<tag>        -> prints tables
+python tools/prof_summary.py gpurun_out/<tag> --md   -> markdown (for profiles/)
+python tools/prof_summary.py gpurun_out/<tag> --traffic-json profiles/pmc_traffic.json --kernel render_kernel
+"""
+import argparse
+import glob
+import json
+import os
+import sqlite3
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "")[:60]
+
+
+def kernel_stats(db):
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, total_calls, total_duration, average, percentage from top_kernels").fetchall()
+    return [(short(r[0]), r[1], r[2], r[3], r[4]) for r in rows]
+
+
+def pmc(db):
+    c = sqlite3.connect(db)
+    q = ("select kernel_name, counter_name, count(*), avg(value), sum(value) from counters_collection "
+         "group by kernel_name, counter_name")
+    return [(short(r[0]), r[1], r[2], r[3], r[4]) for r in c.execute(q).fetchall()]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--md", action="store_true")
+    ap.add_argument("--traffic-json")
+    ap.add_argument("--kernel", default="render_kernel")
+    a = ap.parse_args()
+    out = []
+    for db in sorted(glob.glob(os.path.join(a.dir, "**", "*.db"), recursive=True)):
+        sub = os.path.relpath(db, a.dir)
+        c = sqlite3.connect(db)
+        has_pmc = c.execute("select count(*) from counters_collection").fetchone()[0] > 0
+        if has_pmc:
+            out.append(f"\n### PMC {sub}\n\n| kernel | counter | dispatches | avg per dispatch |\n|---|---|---|---|")
+            for k, cn, n, avg, _ in pmc(db):
+                if k.startswith(("at::", "__amd")):
+                    continue
+                out.append(f"| {k} | {cn} | {n} | {avg:.1f} |")
+        else:
+            out.append(f"\n### kernel trace {sub}\n\n| kernel | calls | total ns | avg ns | % |\n|---|---|---|---|---|")
+            for k, n, tot, avg, pct in kernel_stats(db):
+                out.append(f"| {k} | {n} | {tot:.0f} | {avg:.1f} | {pct:.2f} |")
+    print("\n".join(out))
+    if a.traffic_json:
+        # FETCH_SIZE / WRITE_SIZE are KiB per dispatch; gfx950 FETCH_SIZE counts half of wide
+        # coalesced reads (MI355X_MICROARCH.md, HBM section) -> doubled.
+        fetch = write = None
+        for db in glob.glob(os.path.join(a.dir, "**", "*.db"), recursive=True):
+            for k, cn, n, avg, _ in pmc(db):
+                if k == a.kernel and cn == "FETCH_SIZE":
+                    fetch = avg * 1024 * 2
+                if k == a.kernel and cn == "WRITE_SIZE":
+                    write = avg * 1024
+        data = {}
+        if os.path.exists(a.traffic_json):
+            data = json.load(open(a.traffic_json))
+        if fetch is not None and write is not None:
+            data[a.kernel] = {"bytes_per_launch": round(fetch + write), "read_bytes": round(fetch),
+                              "write_bytes": round(write), "source": a.dir,
+                              "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->B"}
+            json.dump(data, open(a.traffic_json, "w"), indent=1)
+            print("traffic", a.kernel, data[a.kernel])
+
+
+if __name__ == "__main__":
+    main()
