@@ -17,8 +17,12 @@ struct RenderOut {
 
 hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream_t st);
 hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, const uint8_t *mask, hipStream_t st);
-hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, int max_steps, int auto_reset,
-                          const uint8_t *actions, float *reward, uint8_t *done, double *eval_score, hipStream_t st);
+// LDS-resident substeps: per-env slot caps of the task and envs per workgroup (blk = 0: state stays in HBM)
+struct StepCaps { int nb, ns, nc, na, blk; };
+size_t mg_step_lds_bytes(const StepCaps &c, int blk);
+hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, const StepCaps &caps, int max_steps,
+                          int auto_reset, const uint8_t *actions, float *reward, uint8_t *done, double *eval_score,
+                          hipStream_t st);
 hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderOut &ro, int mode, hipStream_t st);
 // profiling builds (-DMG_PROFILE): copy and clear each translation unit's phase timers
 hipError_t mg_prof_read_physics(unsigned long long *out64);

@@ -13,10 +13,10 @@
 #include "mg_math.h"
 #include "mg_state.h"
 
-#define AT(p, i) (p)[(size_t)(i) * (size_t)S.N + (size_t)e]
-#define CPA(k, c) S.cp[((size_t)(k) * MG_MAX_CONS + (size_t)(c)) * (size_t)S.N + (size_t)e]
-#define ACON(k, f, a) S.acon[(((size_t)(k) * AC_NUM + (size_t)(f)) * MG_MAX_ARB + (size_t)(a)) * (size_t)S.N + (size_t)e]
-#define AHASH(k, a) S.ahash[((size_t)(k) * MG_MAX_ARB + (size_t)(a)) * (size_t)S.N + (size_t)e]
+#define AT(p, i) (p)[(uint32_t)(i) * (uint32_t)S.N + (uint32_t)e]
+#define CPA(k, c) S.cp[((uint32_t)(k) * (uint32_t)S.cons_cap + (uint32_t)(c)) * (uint32_t)S.N + (uint32_t)e]
+#define ACON(k, f, a) S.acon[(((uint32_t)(k) * AC_NUM + (uint32_t)(f)) * (uint32_t)S.arb_cap + (uint32_t)(a)) * (uint32_t)S.N + (uint32_t)e]
+#define AHASH(k, a) S.ahash[((uint32_t)(k) * (uint32_t)S.arb_cap + (uint32_t)(a)) * (uint32_t)S.N + (uint32_t)e]
 
 struct V2 { double x, y; };
 MG_DEV V2 v2(double x, double y) { return {x, y}; }

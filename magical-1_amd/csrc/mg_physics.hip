@@ -19,21 +19,116 @@ __global__ void __launch_bounds__(64) reset_kernel(MGState S, const mg_library *
     reset_env(S, L, e, cfg);
 }
 
-__global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg, int max_steps,
-                                                  int auto_reset, const uint8_t *__restrict__ actions, float *reward,
-                                                  uint8_t *done, double *eval_score) {
-    int e = blockIdx.x * blockDim.x + threadIdx.x;
+// ---- LDS-resident substeps ------------------------------------------------
+// The 10 substeps of an env-step touch only the env's bodies, shapes,
+// constraints, arbiters and a few scalars.  They are copied once per env-step
+// from HBM ([slot][N] arrays) into LDS ([slot][BLK] arrays, one column per lane)
+// and the MGState "view" V points there with V.N = BLK and e = lane, so the same
+// device code runs against LDS; everything is copied back before scoring and
+// the in-place reset (which use the HBM state).  A lane only touches its own
+// column, so no barrier is needed.
+template <typename T>
+__device__ __forceinline__ T *carve(unsigned char *base, size_t &off, size_t count) {
+    off = (off + 15) & ~(size_t)15;
+    T *p = (T *)(base + off);
+    off += count * sizeof(T);
+    return p;
+}
+
+__device__ __forceinline__ void carve_view(MGState &V, unsigned char *smem, const StepCaps &c, int blk) {
+    size_t off = 0;
+    const size_t B = (size_t)c.nb * blk, SH = (size_t)c.ns * blk, C = (size_t)c.nc * blk, A = (size_t)c.na * blk;
+    V.bpx = carve<double>(smem, off, B); V.bpy = carve<double>(smem, off, B); V.bvx = carve<double>(smem, off, B);
+    V.bvy = carve<double>(smem, off, B); V.ba = carve<double>(smem, off, B); V.bw = carve<double>(smem, off, B);
+    V.bvbx = carve<double>(smem, off, B); V.bvby = carve<double>(smem, off, B); V.bwb = carve<double>(smem, off, B);
+    V.brc = carve<double>(smem, off, B); V.brs = carve<double>(smem, off, B); V.bminv = carve<double>(smem, off, B);
+    V.biinv = carve<double>(smem, off, B); V.bacache = carve<double>(smem, off, B);
+    V.sr = carve<double>(smem, off, SH); V.su = carve<double>(smem, off, SH); V.sbbl = carve<double>(smem, off, SH);
+    V.sbbb = carve<double>(smem, off, SH); V.sbbr = carve<double>(smem, off, SH); V.sbbt = carve<double>(smem, off, SH);
+    V.cp = carve<double>(smem, off, (size_t)CP_NUM * C);
+    V.anx = carve<double>(smem, off, A); V.any = carve<double>(smem, off, A); V.au = carve<double>(smem, off, A);
+    V.acon = carve<double>(smem, off, (size_t)2 * AC_NUM * A); V.ahash = carve<uint64_t>(smem, off, 2 * A);
+    V.curr_dt = carve<double>(smem, off, blk); V.target_speed = carve<double>(smem, off, blk);
+    V.rel_turn = carve<double>(smem, off, blk); V.target_finger = carve<double>(smem, off, blk);
+    V.akey = carve<int32_t>(smem, off, A); V.astamp = carve<uint32_t>(smem, off, A);
+    V.nbodies = carve<int32_t>(smem, off, blk); V.nshapes = carve<int32_t>(smem, off, blk);
+    V.ncons = carve<int32_t>(smem, off, blk); V.nactive = carve<int32_t>(smem, off, blk);
+    V.stamp = carve<uint32_t>(smem, off, blk); V.overflow = carve<int32_t>(smem, off, blk);
+    V.robot_body0 = carve<int32_t>(smem, off, blk); V.robot_cons0 = carve<int32_t>(smem, off, blk);
+    V.sgroup = carve<int16_t>(smem, off, SH); V.shash = carve<int16_t>(smem, off, SH);
+    V.sbody = carve<int8_t>(smem, off, SH); V.spoly = carve<int8_t>(smem, off, SH);
+    V.ctype = carve<int8_t>(smem, off, C); V.ca = carve<int8_t>(smem, off, C); V.cb = carve<int8_t>(smem, off, C);
+    V.astate = carve<int8_t>(smem, off, A); V.acount = carve<int8_t>(smem, off, A); V.asa = carve<int8_t>(smem, off, A);
+    V.asb = carve<int8_t>(smem, off, A); V.active = carve<int8_t>(smem, off, A);
+    V.N = blk;
+    V.cons_cap = c.nc;
+    V.arb_cap = c.na;
+}
+
+// rows [0, rows) of a [row][N] HBM array <-> [row][BLK] LDS array (lane's column); for the
+// cp / acon / ahash blocks the HBM row of LDS row (k, r) is k * hcap + r
+template <typename T>
+__device__ __forceinline__ void xfer(T *lds, T *hbm, int rows, int blk, int lane, int N, int e, bool to_lds,
+                                     int groups = 1, int lcap = 0, int hcap = 0) {
+    for (int g = 0; g < groups; g++)
+        for (int r = 0; r < rows; r++) {
+            const uint32_t li = (uint32_t)(g * lcap + r) * blk + lane, hi = (uint32_t)(g * hcap + r) * N + e;
+            if (to_lds) lds[li] = hbm[hi]; else hbm[hi] = lds[li];
+        }
+}
+
+__device__ __forceinline__ void xfer_state(const MGState &S, const MGState &V, const StepCaps &c, int lane, int e,
+                                           bool in) {
+    const int blk = V.N, N = S.N;
+#define XF(f, rows) xfer(V.f, S.f, rows, blk, lane, N, e, in)
+    XF(bpx, c.nb); XF(bpy, c.nb); XF(bvx, c.nb); XF(bvy, c.nb); XF(ba, c.nb); XF(bw, c.nb); XF(bvbx, c.nb);
+    XF(bvby, c.nb); XF(bwb, c.nb); XF(brc, c.nb); XF(brs, c.nb); XF(bacache, c.nb);
+    XF(sbbl, c.ns); XF(sbbb, c.ns); XF(sbbr, c.ns); XF(sbbt, c.ns);
+    xfer(V.cp, S.cp, c.nc, blk, lane, N, e, in, CP_NUM, c.nc, MG_MAX_CONS);
+    XF(anx, c.na); XF(any, c.na); XF(au, c.na); XF(akey, c.na); XF(astamp, c.na);
+    XF(astate, c.na); XF(acount, c.na); XF(asa, c.na); XF(asb, c.na); XF(active, c.na);
+    xfer(V.acon, S.acon, c.na, blk, lane, N, e, in, 2 * AC_NUM, c.na, MG_MAX_ARB);
+    xfer(V.ahash, S.ahash, c.na, blk, lane, N, e, in, 2, c.na, MG_MAX_ARB);
+    XF(curr_dt, 1); XF(target_speed, 1); XF(rel_turn, 1); XF(target_finger, 1);
+    XF(nactive, 1); XF(stamp, 1); XF(overflow, 1);
+    if (in) { // read-only during the substeps
+        XF(bminv, c.nb); XF(biinv, c.nb);
+        XF(sr, c.ns); XF(su, c.ns); XF(sgroup, c.ns); XF(shash, c.ns); XF(sbody, c.ns); XF(spoly, c.ns);
+        XF(ctype, c.nc); XF(ca, c.nc); XF(cb, c.nc);
+        XF(nbodies, 1); XF(nshapes, 1); XF(ncons, 1); XF(robot_body0, 1); XF(robot_cons0, 1);
+    }
+#undef XF
+}
+
+template <bool LDS>
+__global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg, StepCaps caps,
+                                                  int max_steps, int auto_reset, const uint8_t *__restrict__ actions,
+                                                  float *reward, uint8_t *done, double *eval_score) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int lane = threadIdx.x, e = blockIdx.x * blockDim.x + lane;
     if (e >= S.n_envs) return;
-    int a = actions[e];
-    robot_set_action(S, L, e, a < 18 ? a : 0);
+    MGState V = S;
+    int ev = e;
+    if (LDS) {
+        if (S.nbodies[e] > caps.nb || S.nshapes[e] > caps.ns || S.ncons[e] > caps.nc) {
+            S.overflow[e] |= 16; // scene larger than the task's LDS caps (never expected)
+            return;
+        }
+        carve_view(V, smem, caps, blockDim.x);
+        xfer_state(S, V, caps, lane, e, true);
+        ev = lane;
+    }
+    const int a = actions[e];
+    robot_set_action(V, L, ev, a < 18 ? a : 0);
     const double dt = L->dt;
     MGProf P;
     MG_PP_INIT(P);
     for (int i = 0; i < 10; i++) {
-        robot_update(S, L, e);
+        robot_update(V, L, ev);
         MG_PP(P, 0);
-        space_step(S, L, e, dt, P);
+        space_step(V, L, ev, dt, P);
     }
+    if (LDS) xfer_state(S, V, caps, lane, e, false);
     int steps = S.episode_steps[e] + 1;
     S.episode_steps[e] = steps;
     bool d = max_steps > 0 && steps >= max_steps;
@@ -46,6 +141,24 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
     MG_PP_END(P, (threadIdx.x & 63) == 0, 32);
 }
 
+// LDS bytes of one env's view (same carve order as carve_view, per-lane columns)
+size_t mg_step_lds_bytes(const StepCaps &c, int blk) {
+    size_t off = 0;
+    auto take = [&](size_t count, size_t size) { off = (off + 15) & ~(size_t)15; off += count * size; };
+    const size_t B = (size_t)c.nb * blk, SH = (size_t)c.ns * blk, C = (size_t)c.nc * blk, A = (size_t)c.na * blk;
+    for (int i = 0; i < 14; i++) take(B, 8);
+    for (int i = 0; i < 6; i++) take(SH, 8);
+    take((size_t)CP_NUM * C, 8);
+    for (int i = 0; i < 3; i++) take(A, 8);
+    take((size_t)2 * AC_NUM * A, 8); take(2 * A, 8);
+    for (int i = 0; i < 4; i++) take(blk, 8);
+    take(A, 4); take(A, 4);
+    for (int i = 0; i < 8; i++) take(blk, 4);
+    take(SH, 2); take(SH, 2); take(SH, 1); take(SH, 1);
+    for (int i = 0; i < 3; i++) take(C, 1);
+    for (int i = 0; i < 5; i++) take(A, 1);
+    return (off + 15) & ~(size_t)15;
+}
 
 static int grid64(const MGState &S) { return (S.n_envs + 63) / 64; }
 
@@ -59,10 +172,24 @@ hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, c
     return hipGetLastError();
 }
 
-hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, int max_steps, int auto_reset,
-                          const uint8_t *actions, float *reward, uint8_t *done, double *eval_score, hipStream_t st) {
-    hipLaunchKernelGGL(step_kernel, dim3(grid64(S)), dim3(64), 0, st, S, L, cfg, max_steps, auto_reset, actions, reward,
-                       done, eval_score);
+hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, const StepCaps &caps, int max_steps,
+                          int auto_reset, const uint8_t *actions, float *reward, uint8_t *done, double *eval_score,
+                          hipStream_t st) {
+    if (caps.blk > 0) {
+        static bool attr_set = false;
+        const size_t lds = mg_step_lds_bytes(caps, caps.blk);
+        if (!attr_set) {
+            hipError_t err = hipFuncSetAttribute((const void *)step_kernel<true>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (err != hipSuccess) return err;
+            attr_set = true;
+        }
+        hipLaunchKernelGGL(step_kernel<true>, dim3((S.n_envs + caps.blk - 1) / caps.blk), dim3(caps.blk), lds, st, S, L,
+                           cfg, caps, max_steps, auto_reset, actions, reward, done, eval_score);
+    } else {
+        hipLaunchKernelGGL(step_kernel<false>, dim3(grid64(S)), dim3(64), 0, st, S, L, cfg, caps, max_steps, auto_reset,
+                           actions, reward, done, eval_score);
+    }
     return hipGetLastError();
 }
 

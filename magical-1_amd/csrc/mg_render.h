@@ -5,8 +5,10 @@
 // surfarray) and benchmarks/__init__.py:150-190 (cv2.resize INTER_AREA 4x).
 //
 // The 384x384 frame never leaves the CU.  Setup (per workgroup) turns the
-// scene into integer vertices, per-row fill spans (pygame draw_fillpoly) and a
-// per-band list of outline segments.  The frame is then produced in 8-row bands:
+// scene into integer vertices (pygame truncation), the two y-monotone vertex
+// chains of every convex polygon, and per-band lists of outline items.  The
+// frame is then produced in 8-row bands: fill spans of the band's rows are found
+// by binary search on the chains (pygame draw_fillpoly's intersection rule),
 // outline pixels go to an LDS layer by atomicMax(draw ordinal) -- the painter's
 // rule "last primitive drawn wins" is "largest ordinal wins" -- and one thread
 // per 4x4 block resolves fills (geoms in draw order), takes the max with the
@@ -19,21 +21,18 @@
 #include "mg_prof.h"
 
 #define RG_MAXG 160
-#define RG_MAXVERT 2048
-#define RG_MAXSPAN 6144
-#define RG_MAXDASH 384
+#define RG_MAXVERT 1600
+#define RG_MAXDASH 256
 #define RG_MAXBIN 2048
 #define RG_MAXLONG 64
 #define RG_BAND 8
 #define RG_NBANDS (MG_RES / RG_BAND)
 #define RG_THREADS 192                  // = one thread per 4x4 block of a band (2 x 96)
 #define RG_SHORT 16                     // segments with <= RG_SHORT pixels in a band: drawn by their own thread
-#define RG_SPAN_SHORT 24                // fill edges spanning <= RG_SPAN_SHORT rows: one thread
 #define RG_EMPTY 32767
 #define RG_LOROW (MG_LORES * 3)         // bytes of one 96-px RGB row
 #define RG_BANDLO (2 * RG_LOROW)        // bytes of the 2 LoRes rows one band produces
 #define RG_BANDLO16 (RG_BANDLO / 16)    // ... in 16-byte chunks (36)
-
 
 // A pygame drawline pixel run in k-form: the major axis has n = max(|dx|,|dy|) + 1
 // pixels and the minor offset of pixel k is m = floor(k * dminor / dmajor) with
@@ -42,8 +41,8 @@
 // y-major: (x1 + sgx*m, y1 + sgy*k).
 struct LineK { int x1, y1, sgx, sgy, DX, DY, xmaj; };
 
-// LDS: the setup matrices, the span bookkeeping and the band buffers are never
-// live at the same time, so they share storage.
+// LDS: the setup matrices and the band buffers are never live at the same time,
+// so they share storage.  Sized for 3 workgroups per CU.
 struct RenderSmem {
     union alignas(16) {
         struct {
@@ -52,10 +51,6 @@ struct RenderSmem {
             double view[9];
         } pre;
         struct {
-            uint32_t scnt[RG_MAXSPAN / 4];  // per span row: #side-A (low nibble) / #side-B (high) intersections
-            int16_t lspan[256];             // fill edges spanning many rows (processed cooperatively)
-        } mid;
-        struct {
             uint32_t band[RG_BAND][MG_RES]; // outline layer of the current band
             uint4 lo[RG_BANDLO16];          // current frame, 2 LoRes rows
             uint4 past[3][RG_BANDLO16];     // frames t-3, t-2, t-1 of the same rows
@@ -63,25 +58,23 @@ struct RenderSmem {
             int32_t lkr[RG_MAXLONG][3];     // klo, khi, ordinal
         } post;
     } u;
+    uint4 ginfo[RG_MAXG];                     // (ymin|ymax<<16, xmin|xmax<<16, top|bot<<16, v0|n<<16)
+    uint32_t bspan[RG_MAXG][RG_BAND];         // spans of the band's rows, per band-list slot: l | r << 16
+    uint64_t col[2 * RG_MAXG + 2];            // R | G << 16 | B << 32 per ordinal
     int16_t g_rpoly[RG_MAXG], g_voff[RG_MAXG + 1], g_nv[RG_MAXG];
-    int16_t g_ymin[RG_MAXG], g_ymax[RG_MAXG], g_xmin[RG_MAXG], g_xmax[RG_MAXG];
     int8_t g_ent[RG_MAXG];
-    int32_t g_soff[RG_MAXG + 1];
     int16_t e_g0[MG_MAX_ENTS + 1];
-    int16_t vx[RG_MAXVERT], vy[RG_MAXVERT];   // int pixel vertices (fill, line ends)
-    int16_t fx[RG_MAXVERT], fy[RG_MAXVERT];   // float->int first points of solid outline edges
+    int16_t vx[RG_MAXVERT], vy[RG_MAXVERT];   // int pixel vertices (pygame (int) truncation)
+    uint8_t fdelta[RG_MAXVERT];               // float->int minus double->int of x (bits 0-1) / y (2-3), +1
     uint8_t v_geom[RG_MAXVERT];
     uint16_t sedge[RG_MAXVERT];               // solid outline edges: start vertex | last << 14 | inside << 15
-    int16_t span[RG_MAXSPAN][2];              // fill intersections of the two y-monotone chains
-    uint4 ginfo[RG_MAXG];                     // (ymin|ymax<<16, xmin|xmax<<16, span base, fill ordinal)
     int16_t blist[RG_MAXG];                   // geoms overlapping the current band, in draw order
     int16_t dash[RG_MAXDASH][4];              // clipped dashed-outline lines
     int16_t dash_o[RG_MAXDASH];
     int16_t bin_off[RG_NBANDS + 1];           // per-band outline item lists
     int32_t bin_cnt[RG_NBANDS];
     int16_t bin[RG_MAXBIN];
-    uint64_t col[2 * RG_MAXG + 2];            // R | G << 16 | B << 32 per ordinal
-    int32_t ngeom, nvert, nspan, nsedge, ndash, nlspan, nlong, nblist, err;
+    int32_t ngeom, nsedge, ndash, nlong, nblist, err;
 #ifdef MG_PROFILE
     unsigned int pw[4];
 #endif
@@ -279,7 +272,9 @@ MG_DEV void edge_ends(const RenderSmem &sm, int k, int &x1, int &y1, int &x2, in
     const uint32_t se = sm.sedge[k];
     const int v = se & 0x3FFF, g = sm.v_geom[v];
     const int nx = (se & 0x4000u) ? v + 1 - sm.g_nv[g] : v + 1;
-    x1 = sm.fx[v]; y1 = sm.fy[v]; x2 = sm.vx[nx]; y2 = sm.vy[nx];
+    const int fd = sm.fdelta[v];
+    x1 = sm.vx[v] + (fd & 3) - 1; y1 = sm.vy[v] + ((fd >> 2) & 3) - 1;
+    x2 = sm.vx[nx]; y2 = sm.vy[nx];
     ord = 2 * g + 2;
     inside = (se & 0x8000u) != 0;
 }
@@ -298,6 +293,29 @@ MG_DEV void item_rows(const RenderSmem &sm, int i, int &ylo, int &yhi) {
         ylo = d[1] < d[3] ? d[1] : d[3];
         yhi = d[1] > d[3] ? d[1] : d[3];
     }
+}
+
+// pygame draw_fillpoly intersection of row y with one y-monotone chain of a convex polygon:
+// the chain edge with ya <= y < yb (or, on the last row, ya < y == yb), x = (y-ya)*(xb-xa)/(yb-ya)+xa.
+// The chain runs from the top vertex to the bottom vertex in direction dir (+1 / -1).
+MG_DEV int chain_x(const RenderSmem &sm, int v0, int n, int top, int bot, int dir, int y, int ymax) {
+    int len = dir > 0 ? bot - top : top - bot;
+    len = (len < 0 ? len + n : len) + 1;
+    // vertex index of chain position j (one wrap at most: j < n)
+    auto cv = [&](int j) { int i = top + dir * j; i = i >= n ? i - n : (i < 0 ? i + n : i); return v0 + i; };
+    int lo, hi;
+    if (y < ymax) { // largest j in [0, len-2] with y_j <= y
+        lo = 0; hi = len - 2;
+        while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (sm.vy[cv(mid)] <= y) lo = mid; else hi = mid - 1; }
+    } else {        // smallest j with y_j == ymax; the edge entering it
+        lo = 1; hi = len - 1;
+        while (lo < hi) { int mid = (lo + hi) >> 1; if (sm.vy[cv(mid)] >= y) hi = mid; else lo = mid + 1; }
+        lo -= 1;
+    }
+    const int a = cv(lo), b = cv(lo + 1);
+    const int ya = sm.vy[a], yb = sm.vy[b], xa = sm.vx[a], xb = sm.vx[b];
+    if (!(ya <= y && (y < yb || (y == ymax && ya < y && y <= yb)))) return RG_EMPTY;
+    return (y - ya) * (xb - xa) / (yb - ya) + xa;
 }
 
 // render polygon point i (local coordinates); the goal rect is make_rect(w, h) of its entity
@@ -346,7 +364,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         sm.e_g0[tid + 1] = (int16_t)my_nr;
     }
     if (tid == 0) {
-        sm.err = 0; sm.ndash = 0; sm.nsedge = 0; sm.nlspan = 0; sm.nlong = 0;
+        sm.err = 0; sm.ndash = 0; sm.nsedge = 0; sm.nlong = 0;
         sm.col[0] = pack_rgb(L->background);
         sm.e_g0[0] = 0;
     }
@@ -419,12 +437,12 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         const double *M = sm.u.pre.g_m[g];
         double gx = __fma_rn(M[1], y, M[0] * x) + M[2];
         double gy = __fma_rn(M[4], y, M[3] * x) + M[5];
-        sm.vx[v] = (int16_t)(int)gx;
-        sm.vy[v] = (int16_t)(int)gy;
+        const int ix = (int)gx, iy = (int)gy;
+        sm.vx[v] = (int16_t)ix;
+        sm.vy[v] = (int16_t)iy;
+        // lines(): first point via float (pg FloatFromObj), second via int
+        sm.fdelta[v] = (uint8_t)(((int)(float)gx - ix + 1) | (((int)(float)gy - iy + 1) << 2));
         if (rp.outline == MG_OUTLINE_SOLID) {
-            // lines(): first point via float (pg FloatFromObj), second via int
-            sm.fx[v] = (int16_t)(int)(float)gx;
-            sm.fy[v] = (int16_t)(int)(float)gy;
             sm.sedge[atomicAdd(&sm.nsedge, 1)] = (uint16_t)(v | (i + 1 == rp.npts ? 0x4000 : 0));
         } else if (rp.outline == MG_OUTLINE_DASHED) {
             int j = i + 1 == rp.npts ? 0 : i + 1;
@@ -435,20 +453,26 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         }
     }
     RG_SYNC();
-    // ---- 4. per-geom bounding rows / columns; span rows; outline items per band ----
+    // ---- 4. per-geom bounds and chains (top / bottom vertex; both chains must be y-monotone);
+    //         outline items per band ----
     for (int g = tid; g < G; g += RG_THREADS) {
-        int v0 = sm.g_voff[g], n = sm.g_nv[g];
-        int ymin = sm.vy[v0], ymax = ymin, xmin = sm.vx[v0], xmax = xmin;
+        const int v0 = sm.g_voff[g], n = sm.g_nv[g];
+        int ymin = sm.vy[v0], ymax = ymin, xmin = sm.vx[v0], xmax = xmin, top = 0, bot = 0;
         for (int i = 1; i < n; i++) {
             int y = sm.vy[v0 + i], x = sm.vx[v0 + i];
-            ymin = y < ymin ? y : ymin; ymax = y > ymax ? y : ymax;
+            if (y < ymin) { ymin = y; top = i; }
+            if (y > ymax) { ymax = y; bot = i; }
             xmin = x < xmin ? x : xmin; xmax = x > xmax ? x : xmax;
         }
-        sm.g_ymin[g] = (int16_t)ymin; sm.g_ymax[g] = (int16_t)ymax;
-        sm.g_xmin[g] = (int16_t)(xmin > 0 ? xmin : 0);
-        sm.g_xmax[g] = (int16_t)(xmax < MG_RES - 1 ? xmax : MG_RES - 1);
-        int r0 = ymin > 0 ? ymin : 0, r1 = ymax < MG_RES - 1 ? ymax : MG_RES - 1;
-        sm.g_soff[g] = r1 >= r0 ? r1 - r0 + 1 : 0;
+        bool mono = true;
+        for (int i = top, py = ymin; i != bot; ) { i = i + 1 == n ? 0 : i + 1; int y = sm.vy[v0 + i]; mono &= y >= py; py = y; }
+        for (int i = top, py = ymin; i != bot; ) { i = i == 0 ? n - 1 : i - 1; int y = sm.vy[v0 + i]; mono &= y >= py; py = y; }
+        if (!mono) sm.err = 4;
+        xmin = xmin > 0 ? xmin : 0;
+        xmax = xmax < MG_RES - 1 ? xmax : MG_RES - 1;
+        sm.ginfo[g] = make_uint4((uint32_t)(uint16_t)ymin | ((uint32_t)(uint16_t)ymax << 16),
+                                 (uint32_t)(uint16_t)xmin | ((uint32_t)(uint16_t)xmax << 16),
+                                 (uint32_t)top | ((uint32_t)bot << 16), (uint32_t)v0 | ((uint32_t)n << 16));
     }
     if (sm.ndash > RG_MAXDASH) sm.err = 1;
     const int nitems = sm.nsedge + (sm.ndash < RG_MAXDASH ? sm.ndash : RG_MAXDASH);
@@ -467,22 +491,10 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         for (int b = ylo / RG_BAND; b <= yhi / RG_BAND && ylo <= yhi; b++) atomicAdd(&sm.bin_cnt[b], 1);
     }
     RG_SYNC();
-    if (tid < 64) {
-        wave_exclusive_scan(sm.g_soff, sm.g_soff, G, lane);
-        wave_exclusive_scan(sm.bin_cnt, sm.bin_off, RG_NBANDS, lane);
-    }
+    if (tid < 64) wave_exclusive_scan(sm.bin_cnt, sm.bin_off, RG_NBANDS, lane);
     RG_SYNC();
-    const int nspan = sm.g_soff[G];
-    if (nspan > RG_MAXSPAN || sm.bin_off[RG_NBANDS] > RG_MAXBIN) sm.err = 3;
+    if (sm.bin_off[RG_NBANDS] > RG_MAXBIN) sm.err = 3;
     if (tid < RG_NBANDS) sm.bin_cnt[tid] = sm.bin_off[tid];
-    for (int g = tid; g < G; g += RG_THREADS) {
-        const int ymin = sm.g_ymin[g];
-        sm.ginfo[g] = make_uint4((uint32_t)(uint16_t)ymin | ((uint32_t)(uint16_t)sm.g_ymax[g] << 16),
-                                 (uint32_t)(uint16_t)sm.g_xmin[g] | ((uint32_t)(uint16_t)sm.g_xmax[g] << 16),
-                                 (uint32_t)(sm.g_soff[g] - (ymin > 0 ? ymin : 0)), (uint32_t)(2 * g + 1));
-    }
-    for (int s = tid; s < nspan; s += RG_THREADS) { sm.span[s][0] = RG_EMPTY; sm.span[s][1] = RG_EMPTY; }
-    for (int s = tid; s < RG_MAXSPAN / 4; s += RG_THREADS) sm.u.mid.scnt[s] = 0u;
     RG_SYNC();
     if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
     for (int i = tid; i < nitems; i += RG_THREADS) {
@@ -492,59 +504,9 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         for (int b = ylo / RG_BAND; b <= yhi / RG_BAND && ylo <= yhi; b++)
             sm.bin[atomicAdd(&sm.bin_cnt[b], 1)] = (int16_t)i;
     }
-    // ---- 5. fill spans (pygame draw_fillpoly): an edge from vertex i-1 to i with ya < yb meets rows
-    //         ya <= y < yb, plus y == yb when yb is the polygon's max row.  The two y-monotone chains of
-    //         these convex polygons (edges going down / up) give the two intersections of every row. ----
-    for (int v = tid; v < NV; v += RG_THREADS) {
-        const int g = sm.v_geom[v], v0 = sm.g_voff[g], n = sm.g_nv[g];
-        const int ip = v == v0 ? v0 + n - 1 : v - 1;
-        const int ya = sm.vy[ip], yb = sm.vy[v];
-        if (ya == yb) continue;
-        const int ymax = sm.g_ymax[g];
-        const int lo = ya < yb ? ya : yb, hi = ya < yb ? yb : ya;
-        const int r0 = sm.g_ymin[g] > 0 ? sm.g_ymin[g] : 0, r1 = ymax < MG_RES - 1 ? ymax : MG_RES - 1;
-        const int ys = lo > r0 ? lo : r0, ye = (hi == ymax ? hi : hi - 1) < r1 ? (hi == ymax ? hi : hi - 1) : r1;
-        if (ye - ys + 1 > RG_SPAN_SHORT) { int q = atomicAdd(&sm.nlspan, 1); if (q < 256) sm.u.mid.lspan[q] = (int16_t)v; continue; }
-        const int xa = ya < yb ? sm.vx[ip] : sm.vx[v], xb = ya < yb ? sm.vx[v] : sm.vx[ip];
-        const int side = ya < yb ? 0 : 1;
-        const uint32_t inc = ya < yb ? 1u : 16u;
-        const int sb = sm.g_soff[g] - r0;
-        for (int y = ys; y <= ye; y++) {
-            sm.span[sb + y][side] = (int16_t)((y - lo) * (xb - xa) / (hi - lo) + xa);
-            atomicAdd(&sm.u.mid.scnt[(sb + y) >> 2], inc << (8 * ((sb + y) & 3)));
-        }
-    }
-    RG_SYNC();
-    const int nls = sm.nlspan < 256 ? sm.nlspan : 256;
-    if (sm.nlspan > 256) sm.err = 3;
-    for (int q = 0; q < nls; q++) {
-        const int v = sm.u.mid.lspan[q];
-        const int g = sm.v_geom[v], v0 = sm.g_voff[g], n = sm.g_nv[g];
-        const int ip = v == v0 ? v0 + n - 1 : v - 1;
-        const int ya = sm.vy[ip], yb = sm.vy[v], ymax = sm.g_ymax[g];
-        const int lo = ya < yb ? ya : yb, hi = ya < yb ? yb : ya;
-        const int r0 = sm.g_ymin[g] > 0 ? sm.g_ymin[g] : 0, r1 = ymax < MG_RES - 1 ? ymax : MG_RES - 1;
-        const int ys = lo > r0 ? lo : r0, ye = (hi == ymax ? hi : hi - 1) < r1 ? (hi == ymax ? hi : hi - 1) : r1;
-        const int xa = ya < yb ? sm.vx[ip] : sm.vx[v], xb = ya < yb ? sm.vx[v] : sm.vx[ip];
-        const int side = ya < yb ? 0 : 1;
-        const uint32_t inc = ya < yb ? 1u : 16u;
-        const int sb = sm.g_soff[g] - r0;
-        for (int y = ys + tid; y <= ye; y += RG_THREADS) {
-            sm.span[sb + y][side] = (int16_t)((y - lo) * (xb - xa) / (hi - lo) + xa);
-            atomicAdd(&sm.u.mid.scnt[(sb + y) >> 2], inc << (8 * ((sb + y) & 3)));
-        }
-    }
-    RG_SYNC();
-    // every row: no intersection, or exactly one per chain (else the fill assumption is violated)
-    for (int s = tid; s < nspan; s += RG_THREADS) {
-        uint32_t c = (sm.u.mid.scnt[s >> 2] >> (8 * (s & 3))) & 255u;
-        if (c != 0u && c != 17u) sm.err = 4;
-    }
-    RG_SYNC();
-    if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
     const int nsedge = sm.nsedge;
     MG_PROF(0);
-    // ---- 6. bands ----
+    // ---- 5. bands ----
     uint8_t *ring = view == 0 ? S.hist_allo : S.hist_ego;
     const size_t FR = (size_t)MG_LORES * MG_LORES * 3;
     const bool fresh = S.episode_steps[e] == 0;
@@ -593,6 +555,25 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         if (tid < 4) sm.pw[tid] = 0u;
 #endif
         MG_PROF_MARK(t_lines);
+        // fill spans of this band's rows for the listed geoms: two chains per (geom, row)
+        const int nbl = sm.nblist;
+        for (int w = tid; w < nbl * RG_BAND; w += RG_THREADS) {
+            const int slot = w / RG_BAND, r = w % RG_BAND, y = y0 + r;
+            const uint4 gi = sm.ginfo[sm.blist[slot]];
+            const int ymin = (int16_t)(gi.x & 0xFFFF), ymax = (int16_t)(gi.x >> 16);
+            uint32_t sp = (uint32_t)RG_EMPTY | ((uint32_t)RG_EMPTY << 16);
+            if (y >= ymin && y <= ymax && ymin < ymax) {
+                const int top = gi.z & 0xFFFF, bot = gi.z >> 16, v0 = gi.w & 0xFFFF, n = gi.w >> 16;
+                const int xa = chain_x(sm, v0, n, top, bot, 1, y, ymax), xb = chain_x(sm, v0, n, top, bot, -1, y, ymax);
+                if (xa != RG_EMPTY && xb != RG_EMPTY) {
+                    const int l = xa < xb ? xa : xb, rr = xa < xb ? xb : xa;
+                    sp = (uint32_t)(uint16_t)l | ((uint32_t)(uint16_t)rr << 16);
+                } else if (xa != RG_EMPTY || xb != RG_EMPTY) {
+                    sm.err = 4;  // a row met by one chain only: the fill assumption is violated
+                }
+            }
+            sm.bspan[slot][r] = sp;
+        }
         // outline items of this band: solid width-2 edges (clip_and_draw_line_width: base line plus one
         // offset copy, each clipped) and clipped dashed-goal lines
         for (int j = sm.bin_off[band_i] + tid; j < sm.bin_off[band_i + 1]; j += RG_THREADS) {
@@ -617,9 +598,8 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         RG_SYNC();
         const int nlong = sm.nlong;
         if (nlong > 0) {
-            for (int q = 0; q < nlong; q++) {
-                const int32_t *d = q < RG_MAXLONG ? sm.u.post.lk[q] : nullptr;
-                if (!d) break;
+            for (int q = 0; q < nlong && q < RG_MAXLONG; q++) {
+                const int32_t *d = sm.u.post.lk[q];
                 LineK Lk = {d[0], d[1], d[2], d[3], d[4], d[5], d[6]};
                 const uint32_t ord = (uint32_t)sm.u.post.lkr[q][2];
                 const int klo = sm.u.post.lkr[q][0], khi = sm.u.post.lkr[q][1];
@@ -630,47 +610,48 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             RG_SYNC();
         }
         MG_PROF(2);
-        // fill + resolve, one thread per 4x4 block: painter's order over geoms (later fill
-        // wins), max with the outline layer, colour, then the area sum of the block
+        // fill + resolve, one thread per 4x4 block: painter's order over the band's geoms (later
+        // fill wins), max with the outline layer, colour, then the area sum of the block
         uint8_t *lo8 = (uint8_t *)sm.u.post.lo;
         MG_PROF_MARK(t_fill);
         {
-            const int yb = y0 + 4 * oyl;
+            const int yb = 4 * oyl, ya = y0 + yb;
             uint32_t o[4][4];
+#pragma unroll
             for (int r = 0; r < 4; r++)
+#pragma unroll
                 for (int c = 0; c < 4; c++) o[r][c] = 0u;
-            const int nbl = sm.nblist;
-            for (int i = 0; i < nbl; i++) {
-                const uint4 gi = sm.ginfo[sm.blist[i]];
-                const int ymin = (int16_t)(gi.x & 0xFFFF), ymax = (int16_t)(gi.x >> 16);
+            for (int slot = 0; slot < nbl; slot++) {
+                const int g = sm.blist[slot];
+                const uint4 gi = sm.ginfo[g];
                 const int xmin = (int16_t)(gi.y & 0xFFFF), xmax = (int16_t)(gi.y >> 16);
-                if (ymax < yb || ymin > yb + 3 || xmax < x0 || xmin > x0 + 3) continue;
-                const int sbase = (int)gi.z;
-                const uint32_t ord = gi.w;
-                uint32_t sp[4];
-                for (int r = 0; r < 4; r++)
-                    sp[r] = (yb + r >= ymin && yb + r <= ymax) ? *(const uint32_t *)&sm.span[sbase + yb + r][0] : 0u;
+                if (xmax < x0 || xmin > x0 + 3) continue;
+                const uint4 s4 = *(const uint4 *)&sm.bspan[slot][yb];
+                const uint32_t ord = 2 * g + 1;
+#pragma unroll
                 for (int r = 0; r < 4; r++) {
-                    const int y = yb + r;
-                    if (y < ymin || y > ymax) continue;
-                    const int sa = (int16_t)(sp[r] & 0xFFFF), sb = (int16_t)(sp[r] >> 16);
-                    const int l = sa < sb ? sa : sb, rr = sa < sb ? sb : sa;
+                    const uint32_t spr = r == 0 ? s4.x : r == 1 ? s4.y : r == 2 ? s4.z : s4.w;
+                    const int l = (int16_t)(spr & 0xFFFF), rr = (int16_t)(spr >> 16);
+#pragma unroll
                     for (int c = 0; c < 4; c++)
                         if (x0 + c >= l && x0 + c <= rr) o[r][c] = ord;
                 }
             }
+            (void)ya;
             uint64_t sum = 0;
+#pragma unroll
             for (int r = 0; r < 4; r++) {
-                const uint4 lv = *(const uint4 *)&sm.u.post.band[4 * oyl + r][x0];
+                const uint4 lv = *(const uint4 *)&sm.u.post.band[yb + r][x0];
                 o[r][0] = o[r][0] > lv.x ? o[r][0] : lv.x;
                 o[r][1] = o[r][1] > lv.y ? o[r][1] : lv.y;
                 o[r][2] = o[r][2] > lv.z ? o[r][2] : lv.z;
                 o[r][3] = o[r][3] > lv.w ? o[r][3] : lv.w;
+#pragma unroll
                 for (int c = 0; c < 4; c++) sum += sm.col[o[r][c]];
             }
             if (mode == 1) {
                 for (int r = 0; r < 4; r++) {
-                    uint8_t *dst = out.full + ((((size_t)e * 2 + view) * MG_RES + yb + r) * MG_RES + x0) * 3;
+                    uint8_t *dst = out.full + ((((size_t)e * 2 + view) * MG_RES + y0 + yb + r) * MG_RES + x0) * 3;
                     for (int c = 0; c < 4; c++) {
                         const uint64_t cc = sm.col[o[r][c]];
                         dst[3 * c] = (uint8_t)cc; dst[3 * c + 1] = (uint8_t)(cc >> 16); dst[3 * c + 2] = (uint8_t)(cc >> 32);
@@ -691,7 +672,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         MG_PROF(3);
 #ifdef MG_PROFILE
         _pacc[5] += sm.pw[0]; _pacc[6] += sm.pw[1]; _pacc[7] += nlong; _pacc[8] += sm.bin_off[band_i + 1] - sm.bin_off[band_i];
-        _pacc[9] += sm.nblist;
+        _pacc[9] += nbl;
 #endif
         // ring of the last 4 LoRes frames: slot nh (all 4 slots at episode start)
         for (int t = tid; t < (fresh ? 4 : 1) * RG_BANDLO16; t += RG_THREADS) {
@@ -706,6 +687,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             const uint8_t *p8 = (const uint8_t *)sm.u.post.past;
             for (int c = tid; c < 4 * RG_BANDLO16; c += RG_THREADS) {
                 uint8_t b[16];
+#pragma unroll
                 for (int j = 0; j < 16; j++) {
                     int byte = 16 * c + j, px = byte / 12, k = (byte % 12) / 3, ch = byte % 3;
                     int src = px * 3 + ch;
@@ -722,6 +704,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         RG_SYNC();
         MG_PROF(4);
     }
+    if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; }
     if (mode == 0 && tid == 0) S.hist_head[view * S.N + e] = nh;
     MG_PROF_END(16 * view);
 }

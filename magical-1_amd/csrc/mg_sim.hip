@@ -35,6 +35,7 @@ struct mg_sim {
     int task, flags, preproc, max_steps, device, auto_reset;
     mg_buffers out;
     int bound;
+    StepCaps caps;     // LDS-resident substep layout (caps.blk = 0: HBM state)
     // optional per-kernel timing (hipEvents on the launch stream)
     int timing;
     std::vector<hipEvent_t> ev;   // triples: before step_kernel, between kernels, after render_kernel
@@ -138,6 +139,38 @@ static void layout(MGState &S, Carver &c) {
 }
 
 static hipStream_t as_stream(void *s) { return (hipStream_t)s; }
+
+// Per-env slot caps of a (task, variant) for the LDS-resident substeps, and the envs
+// per workgroup: the smallest power of two that covers the envs with <= 256
+// workgroups (one per CU) among those whose LDS view fits in 160 KB.
+static StepCaps step_caps(int task, int flags, int n_envs, const mg_library &lib) {
+    int nblk = 0, star_ok = 1;
+    switch (task) {
+    case MG_TASK_MOVE_TO_REGION: nblk = 0; break;
+    case MG_TASK_MOVE_TO_CORNER: nblk = 1; star_ok = (flags & MG_RAND_SHAPE_TYPE) != 0; break;
+    case MG_TASK_CLUSTER_COLOUR:
+    case MG_TASK_CLUSTER_SHAPE: nblk = (flags & MG_RAND_SHAPE_COUNT) ? 10 : 8; break;
+    default: nblk = (flags & MG_RAND_SHAPE_COUNT) ? 8 : 5; break;
+    }
+    const int per_blk = star_ok ? lib.block_nshapes[MG_SHAPE_STAR] : 1;
+    StepCaps c;
+    c.nb = 6 + nblk;
+    c.ns = 5 + nblk * per_blk;
+    c.nc = 10 + 2 * nblk;
+    int pairs = 4 * c.ns + 5 * (c.ns - 5) + ((c.ns - 5) * (c.ns - 6)) / 2; // walls, robot-block, block-block
+    c.na = pairs < MG_MAX_ARB ? (pairs + 3) / 4 * 4 : MG_MAX_ARB;
+    if (c.nb > MG_MAX_BODIES || c.ns > MG_MAX_SHAPES || c.nc > MG_MAX_CONS) { c.blk = 0; return c; }
+    int target = (n_envs + 255) / 256, best_fit = 0, pick = 0;
+    for (int b = 1; b <= 64; b *= 2) {
+        if (mg_step_lds_bytes(c, b) > 160 * 1024) break;
+        best_fit = b;
+        if (!pick && b >= target) pick = b;
+    }
+    c.blk = pick ? pick : best_fit;
+    const char *ov = getenv("MG_STEP_BLK"); // experiments: 0 = HBM-state kernel, else envs per workgroup
+    if (ov) { int b = atoi(ov); if (b == 0 || (b <= 64 && mg_step_lds_bytes(c, b) <= 160 * 1024)) c.blk = b; }
+    return c;
+}
 static int grid64(const mg_sim *s) { return (s->S.n_envs + 63) / 64; }
 
 static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
@@ -183,6 +216,8 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     s->task = cfg->task; s->flags = cfg->rand_flags; s->preproc = cfg->preproc;
     s->max_steps = cfg->max_episode_steps; s->device = cfg->device; s->auto_reset = cfg->auto_reset;
     s->S.n_envs = cfg->num_envs;
+    s->S.cons_cap = MG_MAX_CONS;
+    s->S.arb_cap = MG_MAX_ARB;
     s->S.N = (cfg->num_envs + 63) / 64 * 64;
     Carver sizing = {nullptr, 0};
     layout(s->S, sizing);
@@ -195,6 +230,7 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     err = hipMalloc((void **)&s->dlib, sizeof(mg_library));
     if (err != hipSuccess) { (void)hipFree(s->pool); delete s; return set_err(-12, "mg_create: hipMalloc library"); }
     HIPC(hipMemcpy(s->dlib, cfg->library, sizeof(mg_library), hipMemcpyHostToDevice));
+    s->caps = step_caps(cfg->task, cfg->rand_flags, cfg->num_envs, *(const mg_library *)cfg->library);
     std::vector<uint32_t> seeds(cfg->num_envs);
     for (int i = 0; i < cfg->num_envs; i++) seeds[i] = cfg->seeds ? cfg->seeds[i] : cfg->base_seed + (uint32_t)i;
     *out = s;
@@ -247,7 +283,7 @@ int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
     hipEvent_t *ev = nullptr;
     if (s->timing && s->ev_used + 3 <= s->ev.size()) { ev = &s->ev[s->ev_used]; s->ev_used += 3; }
     if (ev) HIPC(hipEventRecord(ev[0], st));
-    HIPC(mg_launch_step(s->S, s->dlib, cfg, s->max_steps, s->auto_reset, actions, s->out.reward, s->out.done,
+    HIPC(mg_launch_step(s->S, s->dlib, cfg, s->caps, s->max_steps, s->auto_reset, actions, s->out.reward, s->out.done,
                         s->out.eval_score, st));
     if (ev) HIPC(hipEventRecord(ev[1], st));
     int rc = 0;

@@ -10,8 +10,9 @@
 #include "mg_common.h"
 
 struct MGState {
-    int N;      // padded env count (multiple of 64)
+    int N;      // padded env count (multiple of 64); row stride of every [slot][N] array
     int n_envs; // live env count
+    int cons_cap, arb_cap; // constraint / arbiter slots per env (MG_MAX_* in HBM; smaller in LDS views)
     // ---- bodies [MG_MAX_BODIES][N] ----
     double *bpx, *bpy, *bvx, *bvy, *ba, *bw, *bvbx, *bvby, *bwb, *brc, *brs, *bminv, *biinv, *bacache;
     int8_t *bkin;   // 1 = kinematic

@@ -203,7 +203,7 @@ MG_DEV void cons_apply(const MGState &S, int e, int c, double dt) {
 // ---- arbiters ------------------------------------------------------------
 MG_DEV void arbiter_update(const MGState &S, const mg_library *L, int e, int key, const ShapeW &A, const ShapeW &B,
                            double ua, double ub, const Collision &info) {
-    int na = MG_MAX_ARB, slot = -1, free_slot = -1;
+    int na = S.arb_cap, slot = -1, free_slot = -1;
     for (int i = 0; i < na; i++) {
         int k = AT(S.akey, i);
         if (k == key) { slot = i; break; }
@@ -240,7 +240,7 @@ MG_DEV void arbiter_update(const MGState &S, const mg_library *L, int e, int key
     AT(S.asa, slot) = sa.body; AT(S.asb, slot) = sb.body;
     if (AT(S.astate, slot) == ARB_CACHED) AT(S.astate, slot) = ARB_FIRST;
     int na_ = S.nactive[e];
-    if (na_ < MG_MAX_ARB) { AT(S.active, na_) = slot; S.nactive[e] = na_ + 1; }
+    if (na_ < S.arb_cap) { AT(S.active, na_) = slot; S.nactive[e] = na_ + 1; }
     else S.overflow[e] |= 1;
     AT(S.astamp, slot) = S.stamp[e];
 }
@@ -358,7 +358,7 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
     }
     MG_PP(P, 2);
     // cached arbiter filter
-    for (int i = 0; i < MG_MAX_ARB; i++) {
+    for (int i = 0; i < S.arb_cap; i++) {
         if (AT(S.akey, i) < 0) continue;
         uint32_t ticks = stamp - AT(S.astamp, i);
         if (ticks >= 1 && AT(S.astate, i) != ARB_CACHED) AT(S.astate, i) = ARB_CACHED;

@@ -90,13 +90,8 @@ def test_library_loads_and_exports_every_header_symbol():
 
 
 def test_library_is_gfx950_code_object():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list", "--type=o",
-                          f"--input={native.LIB_PATH}"], capture_output=True, text=True)
-    if out.returncode != 0:
-        data = open(native.LIB_PATH, "rb").read()
-        assert b"gfx950" in data
-    else:
-        assert "gfx950" in out.stdout
+    data = open(native.LIB_PATH, "rb").read()
+    assert b"gfx950" in data  # the embedded offload bundle targets amdgcn-amd-amdhsa--gfx950
 
 
 def test_abi_argument_validation_without_gpu():

@@ -47,7 +47,7 @@ def main():
                     continue
                 out.append(f"| {k} | {cn} | {n} | {avg:.1f} |")
         else:
-            out.append(f"\n### kernel trace {sub}\n\n| kernel | calls | total ns | avg ns | % |\n|---|---|---|---|---|")
+            out.append(f"\n### kernel trace {sub}\n\n| kernel | calls | total us | avg us | % |\n|---|---|---|---|---|")
             for k, n, tot, avg, pct in kernel_stats(db):
                 out.append(f"| {k} | {n} | {tot:.0f} | {avg:.1f} | {pct:.2f} |")
     print("\n".join(out))
