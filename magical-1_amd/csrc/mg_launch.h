@@ -13,6 +13,8 @@ struct RenderOut {
     uint8_t *obs_past;
     const uint8_t *mask;  // reset mask: envs with mask[e] == 0 are left untouched (null: all)
     int preproc;
+    int debug_skip;       // profiling builds only: 1 skip outlines, 2 skip fill, 4 skip HBM stores, 8 skip spans
+    int small;            // 1: robot + arena + goal + one block at most (MoveToRegion, MoveToCorner) -> small LDS class
 };
 
 hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream_t st);

@@ -3,7 +3,10 @@
 #include "mg_render.h"
 
 hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderOut &ro, int mode, hipStream_t st) {
-    hipLaunchKernelGGL(render_kernel, dim3(S.n_envs, 2), dim3(RG_THREADS), 0, st, S, L, ro, mode);
+    if (ro.small)
+        hipLaunchKernelGGL(render_kernel<RenderSmem<RG_SMALL>>, dim3(S.n_envs, 2), dim3(RG_THREADS), 0, st, S, L, ro, mode);
+    else
+        hipLaunchKernelGGL(render_kernel<RenderSmem<RG_LARGE>>, dim3(S.n_envs, 2), dim3(RG_THREADS), 0, st, S, L, ro, mode);
     return hipGetLastError();
 }
 

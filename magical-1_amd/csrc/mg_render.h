@@ -20,10 +20,11 @@
 #include "mg_step.h"
 #include "mg_prof.h"
 
-#define RG_MAXG 160
-#define RG_MAXVERT 1600
-#define RG_MAXDASH 256
-#define RG_MAXBIN 2048
+// capacity classes (template parameters of the LDS layout): geoms, vertices, dash lines, bin entries
+// (outline items + fill edges, binned per band).  The large class fits every task; the small one fits
+// robot + arena + goal + one block (MoveToRegion / MoveToCorner) and leaves room for 5 workgroups/CU.
+#define RG_LARGE 160, 1600, 256, 3072
+#define RG_SMALL 32, 704, 160, 1536
 #define RG_MAXLONG 64
 #define RG_BAND 8
 #define RG_NBANDS (MG_RES / RG_BAND)
@@ -43,7 +44,9 @@ struct LineK { int x1, y1, sgx, sgy, DX, DY, xmaj; };
 
 // LDS: the setup matrices and the band buffers are never live at the same time,
 // so they share storage.  Sized for 3 workgroups per CU.
+template <int MAXG_, int MAXVERT_, int MAXDASH_, int MAXBIN_>
 struct RenderSmem {
+    static constexpr int RG_MAXG = MAXG_, RG_MAXVERT = MAXVERT_, RG_MAXDASH = MAXDASH_, RG_MAXBIN = MAXBIN_;
     union alignas(16) {
         struct {
             double g_m[RG_MAXG][6];
@@ -71,9 +74,11 @@ struct RenderSmem {
     int16_t blist[RG_MAXG];                   // geoms overlapping the current band, in draw order
     int16_t dash[RG_MAXDASH][4];              // clipped dashed-outline lines
     int16_t dash_o[RG_MAXDASH];
-    int16_t bin_off[RG_NBANDS + 1];           // per-band outline item lists
-    int32_t bin_cnt[RG_NBANDS];
+    int16_t bin_off[RG_NBANDS + 1];           // per-band outline item lists (in bin[])
+    int16_t ebin_off[RG_NBANDS + 1];          // per-band fill edge lists (in bin[], after the outline items)
+    int32_t bin_cnt[RG_NBANDS], ebin_cnt[RG_NBANDS];
     int16_t bin[RG_MAXBIN];
+    int16_t gslot[RG_MAXG];                   // band-list slot of each geom overlapping the current band
     int32_t ngeom, nsedge, ndash, nlong, nblist, err;
 #ifdef MG_PROFILE
     unsigned int pw[4];
@@ -128,6 +133,7 @@ MG_DEV int cs_encode(int x, int y) {
 }
 MG_DEV bool clipline(int &x1, int &y1, int &x2, int &y2) {
     const int left = 0, top = 0, right = MG_RES - 1, bottom = MG_RES - 1;
+#pragma unroll 1
     for (int guard = 0; guard < 16; guard++) {
         int code1 = cs_encode(x1, y1), code2 = cs_encode(x2, y2);
         if (!(code1 | code2)) return true;
@@ -146,16 +152,18 @@ MG_DEV bool clipline(int &x1, int &y1, int &x2, int &y2) {
     return false;
 }
 
-MG_DEV void push_line(RenderSmem &sm, int x1, int y1, int x2, int y2, int ord) {
+template <class SM>
+MG_DEV void push_line(SM &sm, int x1, int y1, int x2, int y2, int ord) {
     if (!clipline(x1, y1, x2, y2)) return;
     int i = atomicAdd(&sm.ndash, 1);
-    if (i >= RG_MAXDASH) { sm.err = 1; return; }
+    if (i >= SM::RG_MAXDASH) { sm.err = 1; return; }
     sm.dash[i][0] = (int16_t)x1; sm.dash[i][1] = (int16_t)y1; sm.dash[i][2] = (int16_t)x2; sm.dash[i][3] = (int16_t)y2;
     sm.dash_o[i] = (int16_t)ord;
 }
 
 // clip_and_draw_line_width (pygame 1.9.6): base line + offsets 1, -1, 2, ...
-MG_DEV void push_wide_line(RenderSmem &sm, int x1, int y1, int x2, int y2, int width, int ord) {
+template <class SM>
+MG_DEV void push_wide_line(SM &sm, int x1, int y1, int x2, int y2, int width, int ord) {
     int xinc = 0, yinc = 0;
     if (abs(x1 - x2) > abs(y1 - y2)) yinc = 1; else xinc = 1;
     push_line(sm, x1, y1, x2, y2, ord);
@@ -179,7 +187,8 @@ MG_DEV double np_arange_at(double start, double step, int i) {
 }
 
 // render.py:232-255 dashed goal outline, one polygon edge
-MG_DEV void push_dashes(RenderSmem &sm, double x1, double y1, double x2, double y2, int ord) {
+template <class SM>
+MG_DEV void push_dashes(SM &sm, double x1, double y1, double x2, double y2, int ord) {
     const double dl = 10;
     double sx, stx, sy, sty;
     int nx, ny;
@@ -205,7 +214,8 @@ MG_DEV void push_dashes(RenderSmem &sm, double x1, double y1, double x2, double 
     }
 }
 
-MG_DEV void band_put(RenderSmem &sm, int x, int y, int y0, uint32_t ord) {
+template <class SM>
+MG_DEV void band_put(SM &sm, int x, int y, int y0, uint32_t ord) {
     int r = y - y0;
     if (r >= 0 && r < RG_BAND && x >= 0 && x < MG_RES) atomicMax(&sm.u.post.band[r][x], ord);
 }
@@ -237,7 +247,8 @@ MG_DEV void band_krange(const LineK &L, int y0, int &klo, int &khi) {
 }
 
 // pixels k in [ka, kb] of a segment; the minor offset is stepped incrementally
-MG_DEV void raster_krange(RenderSmem &sm, const LineK &L, int ka, int kb, int y0, uint32_t ord) {
+template <class SM>
+MG_DEV void raster_krange(SM &sm, const LineK &L, int ka, int kb, int y0, uint32_t ord) {
     const int dmaj = L.xmaj ? L.DX : L.DY, dmin = L.xmaj ? L.DY : L.DX;
     const int ax = L.xmaj ? L.sgx : 0, ay = L.xmaj ? 0 : L.sgy;   // per k
     const int bx = L.xmaj ? 0 : L.sgx, by = L.xmaj ? L.sgy : 0;   // per m
@@ -250,7 +261,8 @@ MG_DEV void raster_krange(RenderSmem &sm, const LineK &L, int ka, int kb, int y0
 }
 
 // one clipped segment: short runs are drawn here, long runs are queued for the whole workgroup
-MG_DEV void segment_band(RenderSmem &sm, int x1, int y1, int x2, int y2, uint32_t ord, int y0) {
+template <class SM>
+MG_DEV void segment_band(SM &sm, int x1, int y1, int x2, int y2, uint32_t ord, int y0) {
     int klo, khi;
     const LineK L = line_k(x1, y1, x2, y2);
     band_krange(L, y0, klo, khi);
@@ -268,7 +280,8 @@ MG_DEV void segment_band(RenderSmem &sm, int x1, int y1, int x2, int y2, uint32_
 }
 
 // end points of solid outline edge k: (float->int first point) -> (int next vertex)
-MG_DEV void edge_ends(const RenderSmem &sm, int k, int &x1, int &y1, int &x2, int &y2, uint32_t &ord, bool &inside) {
+template <class SM>
+MG_DEV void edge_ends(const SM &sm, int k, int &x1, int &y1, int &x2, int &y2, uint32_t &ord, bool &inside) {
     const uint32_t se = sm.sedge[k];
     const int v = se & 0x3FFF, g = sm.v_geom[v];
     const int nx = (se & 0x4000u) ? v + 1 - sm.g_nv[g] : v + 1;
@@ -280,7 +293,8 @@ MG_DEV void edge_ends(const RenderSmem &sm, int k, int &x1, int &y1, int &x2, in
 }
 
 // rows covered by outline item i (solid edge sub-lines or a dash line), before clipping
-MG_DEV void item_rows(const RenderSmem &sm, int i, int &ylo, int &yhi) {
+template <class SM>
+MG_DEV void item_rows(const SM &sm, int i, int &ylo, int &yhi) {
     if (i < sm.nsedge) {
         int x1, y1, x2, y2;
         uint32_t ord;
@@ -295,27 +309,24 @@ MG_DEV void item_rows(const RenderSmem &sm, int i, int &ylo, int &yhi) {
     }
 }
 
-// pygame draw_fillpoly intersection of row y with one y-monotone chain of a convex polygon:
-// the chain edge with ya <= y < yb (or, on the last row, ya < y == yb), x = (y-ya)*(xb-xa)/(yb-ya)+xa.
-// The chain runs from the top vertex to the bottom vertex in direction dir (+1 / -1).
-MG_DEV int chain_x(const RenderSmem &sm, int v0, int n, int top, int bot, int dir, int y, int ymax) {
-    int len = dir > 0 ? bot - top : top - bot;
-    len = (len < 0 ? len + n : len) + 1;
-    // vertex index of chain position j (one wrap at most: j < n)
-    auto cv = [&](int j) { int i = top + dir * j; i = i >= n ? i - n : (i < 0 ? i + n : i); return v0 + i; };
-    int lo, hi;
-    if (y < ymax) { // largest j in [0, len-2] with y_j <= y
-        lo = 0; hi = len - 2;
-        while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (sm.vy[cv(mid)] <= y) lo = mid; else hi = mid - 1; }
-    } else {        // smallest j with y_j == ymax; the edge entering it
-        lo = 1; hi = len - 1;
-        while (lo < hi) { int mid = (lo + hi) >> 1; if (sm.vy[cv(mid)] >= y) hi = mid; else lo = mid + 1; }
-        lo -= 1;
-    }
-    const int a = cv(lo), b = cv(lo + 1);
-    const int ya = sm.vy[a], yb = sm.vy[b], xa = sm.vx[a], xb = sm.vx[b];
-    if (!(ya <= y && (y < yb || (y == ymax && ya < y && y <= yb)))) return RG_EMPTY;
-    return (y - ya) * (xb - xa) / (yb - ya) + xa;
+// rows of fill edge (ip -> v) under pygame draw_fillpoly's rule: with (ya, xa) the upper end, the
+// edge meets rows ya <= y < yb, plus y == yb when yb is the polygon's last row; horizontal edges none
+template <class SM>
+MG_DEV void fill_edge(const SM &sm, int ve, int &xa, int &ya, int &xb, int &yb, int &side, int &r0, int &r1) {
+    const int v = ve & 0x3FFF, g = sm.v_geom[v];
+    const int ip = (ve & 0x4000) ? v + sm.g_nv[g] - 1 : v - 1;
+    const uint4 gi = sm.ginfo[g];
+    const int gymin = (int16_t)(gi.x & 0xFFFF), gymax = (int16_t)(gi.x >> 16);
+    const bool onscreen = (int16_t)(gi.y & 0xFFFF) <= (int16_t)(gi.y >> 16); // else never in a band list
+    int y1 = sm.vy[ip], y2 = sm.vy[v];
+    side = y1 < y2 ? 0 : 1;
+    if (y1 < y2) { xa = sm.vx[ip]; ya = y1; xb = sm.vx[v]; yb = y2; }
+    else { xa = sm.vx[v]; ya = y2; xb = sm.vx[ip]; yb = y1; }
+    r0 = ya > 0 ? ya : 0;
+    r1 = yb == gymax ? yb : yb - 1;
+    r1 = r1 < MG_RES - 1 ? r1 : MG_RES - 1;
+    if (y1 == y2 || !onscreen) r1 = r0 - 1;
+    (void)gymin;
 }
 
 // render polygon point i (local coordinates); the goal rect is make_rect(w, h) of its entity
@@ -346,9 +357,10 @@ MG_DEV void entity_xforms(const MGState &S, int e, int ent, double (*xf)[9]) {
 }
 
 // One (env, view) per workgroup.  mode 0: LoRes outputs; mode 1: full-resolution frames.
+template <class SM>
 __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out,
                                                             int mode) {
-    __shared__ RenderSmem sm;
+    __shared__ SM sm;
     const int e = blockIdx.x, view = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
     if (e >= S.n_envs || (out.mask && !out.mask[e])) return;
     MG_PROF_BEGIN(tid == 0);
@@ -368,7 +380,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         sm.col[0] = pack_rgb(L->background);
         sm.e_g0[0] = 0;
     }
-    if (tid < RG_NBANDS) sm.bin_cnt[tid] = 0;
+    if (tid < RG_NBANDS) { sm.bin_cnt[tid] = 0; sm.ebin_cnt[tid] = 0; }
     if (view == 0 && tid == 32) { // Viewer.render: stack.push(self.transform) -> eye(3) @ view
         const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
         mg_mat3_mul(I3, L->allo_view, sm.u.pre.view);
@@ -391,7 +403,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     if (tid == 0) {
         for (int k = 0; k < nents; k++) sm.e_g0[k + 1] += sm.e_g0[k];
         sm.ngeom = sm.e_g0[nents];
-        if (sm.ngeom > RG_MAXG) sm.err = 2;
+        if (sm.ngeom > SM::RG_MAXG) sm.err = 2;
     }
     RG_SYNC();
     if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
@@ -424,7 +436,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     }
     RG_SYNC();
     const int NV = sm.g_voff[G];
-    if (NV > RG_MAXVERT) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
+    if (NV > SM::RG_MAXVERT) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
     for (int g = tid; g < G; g += RG_THREADS)
         for (int i = 0, v0 = sm.g_voff[g]; i < sm.g_nv[g]; i++) sm.v_geom[v0 + i] = (uint8_t)g;
     RG_SYNC();
@@ -474,8 +486,8 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
                                  (uint32_t)(uint16_t)xmin | ((uint32_t)(uint16_t)xmax << 16),
                                  (uint32_t)top | ((uint32_t)bot << 16), (uint32_t)v0 | ((uint32_t)n << 16));
     }
-    if (sm.ndash > RG_MAXDASH) sm.err = 1;
-    const int nitems = sm.nsedge + (sm.ndash < RG_MAXDASH ? sm.ndash : RG_MAXDASH);
+    if (sm.ndash > SM::RG_MAXDASH) sm.err = 1;
+    const int nitems = sm.nsedge + (sm.ndash < SM::RG_MAXDASH ? sm.ndash : SM::RG_MAXDASH);
     for (int i = tid; i < nitems; i += RG_THREADS) {
         int ylo, yhi;
         item_rows(sm, i, ylo, yhi);
@@ -490,11 +502,24 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         ylo = ylo > 0 ? ylo : 0; yhi = yhi < MG_RES - 1 ? yhi : MG_RES - 1;
         for (int b = ylo / RG_BAND; b <= yhi / RG_BAND && ylo <= yhi; b++) atomicAdd(&sm.bin_cnt[b], 1);
     }
+    for (int i = tid; i < SM::RG_MAXG * RG_BAND; i += RG_THREADS)
+        (&sm.bspan[0][0])[i] = (uint32_t)RG_EMPTY | ((uint32_t)RG_EMPTY << 16);
     RG_SYNC();
-    if (tid < 64) wave_exclusive_scan(sm.bin_cnt, sm.bin_off, RG_NBANDS, lane);
+    for (int v = tid; v < NV; v += RG_THREADS) { // fill edges per band (needs the geoms' row ranges)
+        const int ve = v | (v == sm.g_voff[sm.v_geom[v]] ? 0x4000 : 0);
+        int xa, ya, xb, yb, side, r0, r1;
+        fill_edge(sm, ve, xa, ya, xb, yb, side, r0, r1);
+        for (int b = r0 / RG_BAND; b <= r1 / RG_BAND && r0 <= r1; b++) atomicAdd(&sm.ebin_cnt[b], 1);
+    }
     RG_SYNC();
-    if (sm.bin_off[RG_NBANDS] > RG_MAXBIN) sm.err = 3;
-    if (tid < RG_NBANDS) sm.bin_cnt[tid] = sm.bin_off[tid];
+    if (tid < 64) {
+        wave_exclusive_scan(sm.bin_cnt, sm.bin_off, RG_NBANDS, lane);
+        wave_exclusive_scan(sm.ebin_cnt, sm.ebin_off, RG_NBANDS, lane);
+    }
+    RG_SYNC();
+    const int nout = sm.bin_off[RG_NBANDS];
+    if (nout + sm.ebin_off[RG_NBANDS] > SM::RG_MAXBIN) sm.err = 3;
+    if (tid < RG_NBANDS) { sm.bin_cnt[tid] = sm.bin_off[tid]; sm.ebin_cnt[tid] = nout + sm.ebin_off[tid]; }
     RG_SYNC();
     if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
     for (int i = tid; i < nitems; i += RG_THREADS) {
@@ -503,6 +528,13 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         ylo = ylo > 0 ? ylo : 0; yhi = yhi < MG_RES - 1 ? yhi : MG_RES - 1;
         for (int b = ylo / RG_BAND; b <= yhi / RG_BAND && ylo <= yhi; b++)
             sm.bin[atomicAdd(&sm.bin_cnt[b], 1)] = (int16_t)i;
+    }
+    for (int v = tid; v < NV; v += RG_THREADS) {
+        const int ve = v | (v == sm.g_voff[sm.v_geom[v]] ? 0x4000 : 0);
+        int xa, ya, xb, yb, side, r0, r1;
+        fill_edge(sm, ve, xa, ya, xb, yb, side, r0, r1);
+        for (int b = r0 / RG_BAND; b <= r1 / RG_BAND && r0 <= r1; b++)
+            sm.bin[atomicAdd(&sm.ebin_cnt[b], 1)] = (int16_t)ve;
     }
     const int nsedge = sm.nsedge;
     MG_PROF(0);
@@ -544,7 +576,11 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
                     ov = ymax >= y0 && ymin < y0 + RG_BAND && xmin <= xmax;
                 }
                 const uint64_t m = __ballot(ov);
-                if (ov) sm.blist[cnt + __popcll(m & ((1ull << lane) - 1ull))] = (int16_t)g;
+                if (ov) {
+                    const int slot = cnt + __popcll(m & ((1ull << lane) - 1ull));
+                    sm.blist[slot] = (int16_t)g;
+                    sm.gslot[g] = (int16_t)slot;
+                }
                 cnt += __popcll(m);
             }
             if (lane == 0) sm.nblist = cnt;
@@ -553,46 +589,46 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         MG_PROF(1);
 #ifdef MG_PROFILE
         if (tid < 4) sm.pw[tid] = 0u;
+        const int dskip = out.debug_skip;
+#else
+        const int dskip = 0;
 #endif
         MG_PROF_MARK(t_lines);
-        // fill spans of this band's rows for the listed geoms: two chains per (geom, row)
+        // fill spans of this band's rows: each binned fill edge writes its chain's intersection
+        // (side 0: edges going down the vertex order, side 1: going up) of the rows it meets here
         const int nbl = sm.nblist;
-        for (int w = tid; w < nbl * RG_BAND; w += RG_THREADS) {
-            const int slot = w / RG_BAND, r = w % RG_BAND, y = y0 + r;
-            const uint4 gi = sm.ginfo[sm.blist[slot]];
-            const int ymin = (int16_t)(gi.x & 0xFFFF), ymax = (int16_t)(gi.x >> 16);
-            uint32_t sp = (uint32_t)RG_EMPTY | ((uint32_t)RG_EMPTY << 16);
-            if (y >= ymin && y <= ymax && ymin < ymax) {
-                const int top = gi.z & 0xFFFF, bot = gi.z >> 16, v0 = gi.w & 0xFFFF, n = gi.w >> 16;
-                const int xa = chain_x(sm, v0, n, top, bot, 1, y, ymax), xb = chain_x(sm, v0, n, top, bot, -1, y, ymax);
-                if (xa != RG_EMPTY && xb != RG_EMPTY) {
-                    const int l = xa < xb ? xa : xb, rr = xa < xb ? xb : xa;
-                    sp = (uint32_t)(uint16_t)l | ((uint32_t)(uint16_t)rr << 16);
-                } else if (xa != RG_EMPTY || xb != RG_EMPTY) {
-                    sm.err = 4;  // a row met by one chain only: the fill assumption is violated
-                }
-            }
-            sm.bspan[slot][r] = sp;
+        for (int j = sm.ebin_off[band_i] + nout + tid; j < sm.ebin_off[band_i + 1] + nout && !(dskip & 8); j += RG_THREADS) {
+            const int ve = sm.bin[j];
+            int xa, ya, xb, yb, side, r0, r1;
+            fill_edge(sm, ve, xa, ya, xb, yb, side, r0, r1);
+            const int slot = sm.gslot[sm.v_geom[ve & 0x3FFF]];
+            int16_t *col = (int16_t *)&sm.bspan[slot][0] + side;
+            const int ra = r0 > y0 ? r0 : y0, rb = r1 < y0 + RG_BAND - 1 ? r1 : y0 + RG_BAND - 1;
+            for (int y = ra; y <= rb; y++) col[2 * (y - y0)] = (int16_t)((y - ya) * (xb - xa) / (yb - ya) + xa);
         }
         // outline items of this band: solid width-2 edges (clip_and_draw_line_width: base line plus one
         // offset copy, each clipped) and clipped dashed-goal lines
-        for (int j = sm.bin_off[band_i] + tid; j < sm.bin_off[band_i + 1]; j += RG_THREADS) {
-            const int i = sm.bin[j];
+        // (one thread per segment: solid edges contribute two, dash lines one)
+        for (int j2 = 2 * sm.bin_off[band_i] + tid; j2 < 2 * sm.bin_off[band_i + 1] && !(dskip & 1); j2 += RG_THREADS) {
+            const int i = sm.bin[j2 >> 1], c = j2 & 1;
+            int x1, y1, x2, y2;
+            uint32_t ord;
+            bool clip = false;
             if (i < nsedge) {
-                int x1, y1, x2, y2;
-                uint32_t ord;
                 bool inside;
                 edge_ends(sm, i, x1, y1, x2, y2, ord, inside);
                 const bool xmaj = abs(x1 - x2) > abs(y1 - y2);
-#pragma unroll 1
-                for (int c = 0; c < 2; c++) {
-                    int a1 = x1 + (c && !xmaj), b1 = y1 + (c && xmaj), a2 = x2 + (c && !xmaj), b2 = y2 + (c && xmaj);
-                    if (inside || clipline(a1, b1, a2, b2)) segment_band(sm, a1, b1, a2, b2, ord, y0);
-                }
+                const int ox = (c && !xmaj) ? 1 : 0, oy = (c && xmaj) ? 1 : 0;
+                x1 += ox; x2 += ox; y1 += oy; y2 += oy;
+                clip = !inside;
             } else {
+                if (c) continue;
                 const int16_t *d = sm.dash[i - nsedge];
-                segment_band(sm, d[0], d[1], d[2], d[3], (uint32_t)sm.dash_o[i - nsedge], y0);
+                x1 = d[0]; y1 = d[1]; x2 = d[2]; y2 = d[3];
+                ord = (uint32_t)sm.dash_o[i - nsedge];
             }
+            if (clip && !clipline(x1, y1, x2, y2)) continue;
+            segment_band(sm, x1, y1, x2, y2, ord, y0);
         }
         MG_PROF_MAXW(sm.pw[0], t_lines);
         RG_SYNC();
@@ -621,7 +657,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             for (int r = 0; r < 4; r++)
 #pragma unroll
                 for (int c = 0; c < 4; c++) o[r][c] = 0u;
-            for (int slot = 0; slot < nbl; slot++) {
+            for (int slot = 0; slot < ((dskip & 2) ? 0 : nbl); slot++) {
                 const int g = sm.blist[slot];
                 const uint4 gi = sm.ginfo[g];
                 const int xmin = (int16_t)(gi.y & 0xFFFF), xmax = (int16_t)(gi.y >> 16);
@@ -631,7 +667,9 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const uint32_t spr = r == 0 ? s4.x : r == 1 ? s4.y : r == 2 ? s4.z : s4.w;
-                    const int l = (int16_t)(spr & 0xFFFF), rr = (int16_t)(spr >> 16);
+                    const int sa = (int16_t)(spr & 0xFFFF), sb = (int16_t)(spr >> 16);
+                    const int l = sa < sb ? sa : sb, rr = sa < sb ? sb : sa;
+                    if (rr == RG_EMPTY) continue;   // a row needs an intersection on both chains
 #pragma unroll
                     for (int c = 0; c < 4; c++)
                         if (x0 + c >= l && x0 + c <= rr) o[r][c] = ord;
@@ -666,7 +704,12 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             }
         }
         MG_PROF_MAXW(sm.pw[1], t_fill);
-        if (mode == 1) { RG_SYNC(); continue; }
+        if (mode == 1) {
+            RG_SYNC();
+            for (int i = tid; i < nbl * RG_BAND; i += RG_THREADS)
+                (&sm.bspan[0][0])[i] = (uint32_t)RG_EMPTY | ((uint32_t)RG_EMPTY << 16);
+            continue;
+        }
         if (do_pf) sm.u.post.past[tid / RG_BANDLO16][tid % RG_BANDLO16] = pf;
         RG_SYNC();
         MG_PROF(3);
@@ -674,15 +717,17 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         _pacc[5] += sm.pw[0]; _pacc[6] += sm.pw[1]; _pacc[7] += nlong; _pacc[8] += sm.bin_off[band_i + 1] - sm.bin_off[band_i];
         _pacc[9] += nbl;
 #endif
+        for (int i = tid; i < nbl * RG_BAND; i += RG_THREADS)  // band spans back to empty for the next band
+            (&sm.bspan[0][0])[i] = (uint32_t)RG_EMPTY | ((uint32_t)RG_EMPTY << 16);
         // ring of the last 4 LoRes frames: slot nh (all 4 slots at episode start)
-        for (int t = tid; t < (fresh ? 4 : 1) * RG_BANDLO16; t += RG_THREADS) {
+        for (int t = tid; t < (fresh ? 4 : 1) * RG_BANDLO16 && !(dskip & 4); t += RG_THREADS) {
             int sl = fresh ? t / RG_BANDLO16 : nh, c = t % RG_BANDLO16;
             *(uint4 *)(ring + ((size_t)sl * S.N + e) * FR + lrow + 16 * c) = sm.u.post.lo[c];
         }
-        if (plain)
+        if (plain && !(dskip & 4))
             for (int c = tid; c < RG_BANDLO16; c += RG_THREADS)
                 *(uint4 *)(o_plain + (size_t)e * FR + lrow + 16 * c) = sm.u.post.lo[c];
-        if (stacked) {
+        if (stacked && !(dskip & 4)) {
             // FlattenFrameStack: [96][96][12] = frames oldest..newest concatenated per pixel
             const uint8_t *p8 = (const uint8_t *)sm.u.post.past;
             for (int c = tid; c < 4 * RG_BANDLO16; c += RG_THREADS) {

@@ -177,6 +177,11 @@ static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
     RenderOut ro;
     ro.full = nullptr;
     ro.mask = mask;
+    ro.debug_skip = 0;
+    ro.small = s->task == MG_TASK_MOVE_TO_REGION || s->task == MG_TASK_MOVE_TO_CORNER;
+#ifdef MG_PROFILE
+    if (getenv("MG_DEBUG_SKIP")) ro.debug_skip = atoi(getenv("MG_DEBUG_SKIP"));
+#endif
     ro.obs_allo = s->out.obs_allo; ro.obs_ego = s->out.obs_ego; ro.obs_past = s->out.obs_past;
     ro.preproc = s->preproc;
     HIPC(mg_launch_render(s->S, s->dlib, ro, 0, st));
@@ -299,6 +304,7 @@ int mg_render_full(mg_sim *s, uint8_t *out, void *stream) {
     memset(&ro, 0, sizeof(ro));
     ro.full = out;
     ro.preproc = s->preproc;
+    ro.small = s->task == MG_TASK_MOVE_TO_REGION || s->task == MG_TASK_MOVE_TO_CORNER;
     HIPC(mg_launch_render(s->S, s->dlib, ro, 1, as_stream(stream)));
     return 0;
 }
