@@ -19,11 +19,13 @@ struct RenderOut {
 
 hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream_t st);
 hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, const uint8_t *mask, hipStream_t st);
-// LDS-resident substeps: per-env slot caps of the task and envs per workgroup (blk = 0: state stays in HBM)
+// LDS-resident substeps: per-env slot caps of a task and envs per workgroup
 struct StepCaps { int nb, ns, nc, na, blk; };
 size_t mg_step_lds_bytes(const StepCaps &c, int blk);
-hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, const StepCaps &caps, int max_steps,
-                          int auto_reset, const uint8_t *actions, float *reward, uint8_t *done, double *eval_score,
+// compiled LDS variant matching these caps for n_envs (0: the HBM-state kernel)
+int mg_step_variant(const StepCaps &c, int n_envs);
+hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, int variant, int max_steps, int auto_reset,
+                          const uint8_t *actions, float *reward, uint8_t *done, double *eval_score, uint8_t *reset_mask,
                           hipStream_t st);
 hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderOut &ro, int mode, hipStream_t st);
 // profiling builds (-DMG_PROFILE): copy and clear each translation unit's phase timers

@@ -70,7 +70,9 @@ __device__ __forceinline__ void carve_view(MGState &V, unsigned char *smem, cons
 template <typename T>
 __device__ __forceinline__ void xfer(T *lds, T *hbm, int rows, int blk, int lane, int N, int e, bool to_lds,
                                      int groups = 1, int lcap = 0, int hcap = 0) {
+#pragma unroll 1
     for (int g = 0; g < groups; g++)
+#pragma unroll 2
         for (int r = 0; r < rows; r++) {
             const uint32_t li = (uint32_t)(g * lcap + r) * blk + lane, hi = (uint32_t)(g * hcap + r) * N + e;
             if (to_lds) lds[li] = hbm[hi]; else hbm[hi] = lds[li];
@@ -100,22 +102,33 @@ __device__ __forceinline__ void xfer_state(const MGState &S, const MGState &V, c
 #undef XF
 }
 
-template <bool LDS>
-__global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg, StepCaps caps,
-                                                  int max_steps, int auto_reset, const uint8_t *__restrict__ actions,
-                                                  float *reward, uint8_t *done, double *eval_score) {
+// Slot caps of the LDS-resident variants (compile-time, so every LDS address folds to a constant
+// offset from the lane's column): 0 = state stays in HBM.
+__host__ __device__ constexpr StepCaps step_variant_caps(int v) {
+    return v == 1 ? StepCaps{6, 5, 10, 20, 16}    // robot only (MoveToRegion)
+         : v == 2 ? StepCaps{7, 6, 12, 32, 16}    // robot + one single-shape block (MoveToCorner)
+         : StepCaps{0, 0, 0, 0, 0};
+}
+
+template <int VAR>
+__global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg, int max_steps,
+                                                  int auto_reset, const uint8_t *__restrict__ actions, float *reward,
+                                                  uint8_t *done, double *eval_score, uint8_t *reset_mask) {
     extern __shared__ __align__(16) unsigned char smem[];
+    constexpr StepCaps C = step_variant_caps(VAR);
+    constexpr bool LDS = VAR != 0;
     const int lane = threadIdx.x, e = blockIdx.x * blockDim.x + lane;
     if (e >= S.n_envs) return;
     MGState V = S;
     int ev = e;
     if (LDS) {
-        if (S.nbodies[e] > caps.nb || S.nshapes[e] > caps.ns || S.ncons[e] > caps.nc) {
-            S.overflow[e] |= 16; // scene larger than the task's LDS caps (never expected)
+        if (S.nbodies[e] > C.nb || S.nshapes[e] > C.ns || S.ncons[e] > C.nc) {
+            S.overflow[e] |= 16; // scene larger than the variant's LDS caps (never expected)
+            if (reset_mask) reset_mask[e] = 0;
             return;
         }
-        carve_view(V, smem, caps, blockDim.x);
-        xfer_state(S, V, caps, lane, e, true);
+        carve_view(V, smem, C, C.blk);
+        xfer_state(S, V, C, lane, e, true);
         ev = lane;
     }
     const int a = actions[e];
@@ -128,7 +141,7 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
         MG_PP(P, 0);
         space_step(V, L, ev, dt, P);
     }
-    if (LDS) xfer_state(S, V, caps, lane, e, false);
+    if (LDS) xfer_state(S, V, C, lane, e, false);
     int steps = S.episode_steps[e] + 1;
     S.episode_steps[e] = steps;
     bool d = max_steps > 0 && steps >= max_steps;
@@ -136,7 +149,8 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
     if (reward) reward[e] = (float)sc;
     if (done) done[e] = d ? 1 : 0;
     if (eval_score) eval_score[e] = sc;
-    if (d && auto_reset) reset_env(S, L, e, cfg); // VecEnv auto-reset: next obs is the new episode's first frame
+    // VecEnv auto-reset (next obs = first frame of the new episode) runs as reset_kernel on this mask
+    if (reset_mask) reset_mask[e] = (d && auto_reset) ? 1 : 0;
     MG_PP(P, 7);
     MG_PP_END(P, (threadIdx.x & 63) == 0, 32);
 }
@@ -172,25 +186,45 @@ hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, c
     return hipGetLastError();
 }
 
-hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, const StepCaps &caps, int max_steps,
-                          int auto_reset, const uint8_t *actions, float *reward, uint8_t *done, double *eval_score,
-                          hipStream_t st) {
-    if (caps.blk > 0) {
-        static bool attr_set = false;
-        const size_t lds = mg_step_lds_bytes(caps, caps.blk);
-        if (!attr_set) {
-            hipError_t err = hipFuncSetAttribute((const void *)step_kernel<true>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            if (err != hipSuccess) return err;
-            attr_set = true;
-        }
-        hipLaunchKernelGGL(step_kernel<true>, dim3((S.n_envs + caps.blk - 1) / caps.blk), dim3(caps.blk), lds, st, S, L,
-                           cfg, caps, max_steps, auto_reset, actions, reward, done, eval_score);
-    } else {
-        hipLaunchKernelGGL(step_kernel<false>, dim3(grid64(S)), dim3(64), 0, st, S, L, cfg, caps, max_steps, auto_reset,
-                           actions, reward, done, eval_score);
+int mg_step_variant(const StepCaps &c, int n_envs) {
+    for (int v = 1; v <= 2; v++) {
+        const StepCaps k = step_variant_caps(v);
+        if (c.nb == k.nb && c.ns == k.ns && c.nc == k.nc && c.na == k.na && n_envs <= k.blk * 256) return v;
     }
+    return 0;
+}
+
+template <int VAR>
+static hipError_t launch_step_var(const MGState &S, const mg_library *L, TaskCfg cfg, int max_steps, int auto_reset,
+                                  const uint8_t *actions, float *reward, uint8_t *done, double *eval_score,
+                                  uint8_t *reset_mask, hipStream_t st) {
+    constexpr StepCaps C = step_variant_caps(VAR);
+    if (VAR == 0) {
+        hipLaunchKernelGGL(step_kernel<VAR>, dim3((S.n_envs + 63) / 64), dim3(64), 0, st, S, L, cfg, max_steps, auto_reset,
+                           actions, reward, done, eval_score, reset_mask);
+        return hipGetLastError();
+    }
+    static bool attr_set = false;
+    const size_t lds = mg_step_lds_bytes(C, C.blk);
+    if (!attr_set) {
+        hipError_t err = hipFuncSetAttribute((const void *)step_kernel<VAR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds);
+        if (err != hipSuccess) return err;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(step_kernel<VAR>, dim3((S.n_envs + C.blk - 1) / C.blk), dim3(C.blk), lds, st, S, L, cfg, max_steps,
+                       auto_reset, actions, reward, done, eval_score, reset_mask);
     return hipGetLastError();
+}
+
+hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, int variant, int max_steps, int auto_reset,
+                          const uint8_t *actions, float *reward, uint8_t *done, double *eval_score, uint8_t *reset_mask,
+                          hipStream_t st) {
+    switch (variant) {
+    case 1: return launch_step_var<1>(S, L, cfg, max_steps, auto_reset, actions, reward, done, eval_score, reset_mask, st);
+    case 2: return launch_step_var<2>(S, L, cfg, max_steps, auto_reset, actions, reward, done, eval_score, reset_mask, st);
+    default: return launch_step_var<0>(S, L, cfg, max_steps, auto_reset, actions, reward, done, eval_score, reset_mask, st);
+    }
 }
 
 hipError_t mg_prof_read_physics(unsigned long long *out) {

@@ -35,7 +35,9 @@ struct mg_sim {
     int task, flags, preproc, max_steps, device, auto_reset;
     mg_buffers out;
     int bound;
-    StepCaps caps;     // LDS-resident substep layout (caps.blk = 0: HBM state)
+    StepCaps caps;     // the task's per-env slot caps
+    int step_variant;  // compiled LDS-resident step variant (0: HBM state)
+    uint8_t *reset_mask; // device u8[N]: envs to auto-reset after the step
     // optional per-kernel timing (hipEvents on the launch stream)
     int timing;
     std::vector<hipEvent_t> ev;   // triples: before step_kernel, between kernels, after render_kernel
@@ -140,9 +142,7 @@ static void layout(MGState &S, Carver &c) {
 
 static hipStream_t as_stream(void *s) { return (hipStream_t)s; }
 
-// Per-env slot caps of a (task, variant) for the LDS-resident substeps, and the envs
-// per workgroup: the smallest power of two that covers the envs with <= 256
-// workgroups (one per CU) among those whose LDS view fits in 160 KB.
+// Per-env slot caps of a (task, variant): bodies, shapes, constraints, arbiter slots.
 static StepCaps step_caps(int task, int flags, int n_envs, const mg_library &lib) {
     int nblk = 0, star_ok = 1;
     switch (task) {
@@ -159,18 +159,21 @@ static StepCaps step_caps(int task, int flags, int n_envs, const mg_library &lib
     c.nc = 10 + 2 * nblk;
     int pairs = 4 * c.ns + 5 * (c.ns - 5) + ((c.ns - 5) * (c.ns - 6)) / 2; // walls, robot-block, block-block
     c.na = pairs < MG_MAX_ARB ? (pairs + 3) / 4 * 4 : MG_MAX_ARB;
-    if (c.nb > MG_MAX_BODIES || c.ns > MG_MAX_SHAPES || c.nc > MG_MAX_CONS) { c.blk = 0; return c; }
-    int target = (n_envs + 255) / 256, best_fit = 0, pick = 0;
-    for (int b = 1; b <= 64; b *= 2) {
-        if (mg_step_lds_bytes(c, b) > 160 * 1024) break;
-        best_fit = b;
-        if (!pick && b >= target) pick = b;
-    }
-    c.blk = pick ? pick : best_fit;
-    const char *ov = getenv("MG_STEP_BLK"); // experiments: 0 = HBM-state kernel, else envs per workgroup
-    if (ov) { int b = atoi(ov); if (b == 0 || (b <= 64 && mg_step_lds_bytes(c, b) <= 160 * 1024)) c.blk = b; }
+    c.blk = 16;
+    (void)n_envs;
     return c;
 }
+
+// LDS views pay off while every env gets its workgroup in a single round of workgroups (one per CU);
+// otherwise the HBM-state kernel (64 envs/wavefront) wins (measured: ClusterColour-Demo x8192 9.4 ms
+// HBM vs 20 ms LDS; MoveToRegion x4096 1.7 ms LDS vs 3.0 ms HBM).
+static int pick_step_variant(const StepCaps &c, int n_envs) {
+    int v = mg_step_variant(c, n_envs);
+    const char *ov = getenv("MG_STEP_VARIANT"); // experiments: force 0 (HBM) or a compiled variant
+    if (ov) { int w = atoi(ov); if (w == 0 || w == v) v = w; }
+    return v;
+}
+
 static int grid64(const mg_sim *s) { return (s->S.n_envs + 63) / 64; }
 
 static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
@@ -236,6 +239,10 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     if (err != hipSuccess) { (void)hipFree(s->pool); delete s; return set_err(-12, "mg_create: hipMalloc library"); }
     HIPC(hipMemcpy(s->dlib, cfg->library, sizeof(mg_library), hipMemcpyHostToDevice));
     s->caps = step_caps(cfg->task, cfg->rand_flags, cfg->num_envs, *(const mg_library *)cfg->library);
+    s->step_variant = pick_step_variant(s->caps, cfg->num_envs);
+    err = hipMalloc((void **)&s->reset_mask, (size_t)s->S.N);
+    if (err != hipSuccess) { (void)hipFree(s->pool); (void)hipFree(s->dlib); delete s; return set_err(-12, "mg_create: hipMalloc mask"); }
+    HIPC(hipMemset(s->reset_mask, 0, (size_t)s->S.N));
     std::vector<uint32_t> seeds(cfg->num_envs);
     for (int i = 0; i < cfg->num_envs; i++) seeds[i] = cfg->seeds ? cfg->seeds[i] : cfg->base_seed + (uint32_t)i;
     *out = s;
@@ -288,8 +295,9 @@ int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
     hipEvent_t *ev = nullptr;
     if (s->timing && s->ev_used + 3 <= s->ev.size()) { ev = &s->ev[s->ev_used]; s->ev_used += 3; }
     if (ev) HIPC(hipEventRecord(ev[0], st));
-    HIPC(mg_launch_step(s->S, s->dlib, cfg, s->caps, s->max_steps, s->auto_reset, actions, s->out.reward, s->out.done,
-                        s->out.eval_score, st));
+    HIPC(mg_launch_step(s->S, s->dlib, cfg, s->step_variant, s->max_steps, s->auto_reset, actions, s->out.reward,
+                        s->out.done, s->out.eval_score, s->reset_mask, st));
+    if (s->auto_reset) HIPC(mg_launch_reset(s->S, s->dlib, cfg, s->reset_mask, st));
     if (ev) HIPC(hipEventRecord(ev[1], st));
     int rc = 0;
     if (s->preproc != MG_PREPROC_NONE) rc = render_lores(s, st, nullptr);
@@ -373,6 +381,7 @@ void mg_destroy(mg_sim *s) {
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
     (void)hipFree(s->pool);
     (void)hipFree(s->dlib);
+    (void)hipFree(s->reset_mask);
     delete s;
 }
 
