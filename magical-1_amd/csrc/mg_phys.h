@@ -124,10 +124,33 @@ MG_DEV void load_goal(double gx, double gy, double w, double h, uint64_t hashid,
     sh.bbl = l; sh.bbb = bb; sh.bbr = r; sh.bbt = t;
 }
 
+// the shape's cached BB (cpShapeCacheBB), computed as load_shape does but without materialising
+// the world-space vertices
 MG_DEV void shape_update_bb(const MGState &S, const mg_library *L, int e, int k) {
-    ShapeW sh;
-    load_shape(S, L, e, k, 0, sh);
-    AT(S.sbbl, k) = sh.bbl; AT(S.sbbb, k) = sh.bbb; AT(S.sbbr, k) = sh.bbr; AT(S.sbbt, k) = sh.bbt;
+    const int b = AT(S.sbody, k), p = AT(S.spoly, k);
+    const double c = AT(S.brc, b), s = AT(S.brs, b), px = AT(S.bpx, b), py = AT(S.bpy, b), r = AT(S.sr, k);
+    double bl, bb, br, bt;
+    if (p < 0) {
+        const double cx = c * 0.0 + (-s) * 0.0 + px, cy = s * 0.0 + c * 0.0 + py;
+        bl = cx - r; bb = cy - r; br = cx + r; bt = cy + r;
+    } else {
+        double l = INFINITY, rr = -INFINITY, lo = INFINITY, t = -INFINITY;
+        const int n = L->poly_count[p];
+        for (int i = 0; i < n; i++) {
+            const double vx = L->poly_v[p][i][0], vy = L->poly_v[p][i][1];
+            const double x = c * vx + (-s) * vy + px, y = s * vx + c * vy + py;
+            l = cpmin(l, x); rr = cpmax(rr, x); lo = cpmin(lo, y); t = cpmax(t, y);
+        }
+        bl = l - r; bb = lo - r; br = rr + r; bt = t + r;
+    }
+    AT(S.sbbl, k) = bl; AT(S.sbbb, k) = bb; AT(S.sbbr, k) = br; AT(S.sbbt, k) = bt;
+}
+
+// BB of arena wall w (load_wall: segment a-b of radius 1)
+MG_DEV void wall_bb(int w, double &l, double &b, double &r, double &t) {
+    const double ax = MG_WALL[w][0], ay = MG_WALL[w][1], bx = MG_WALL[w][2], by = MG_WALL[w][3];
+    l = (ax < bx ? ax : bx) - 1.0; r = (ax < bx ? bx : ax) + 1.0;
+    b = (ay < by ? ay : by) - 1.0; t = (ay < by ? by : ay) + 1.0;
 }
 
 // --------------------------------------------------------------------------

@@ -79,26 +79,57 @@ __device__ __forceinline__ void xfer(T *lds, T *hbm, int rows, int blk, int lane
         }
 }
 
+// HBM <-> LDS view transfer of what the substeps read (in) / what later env-steps need (out):
+// bodies (incl. bias velocities and the rotation cache), the constraints' parameters and
+// warm-start impulses, the live arbiters (key, contacts, warm-start hashes) and the active list.
+// Cached shape BBs and the constraints' pre-step products are recomputed before use.
 __device__ __forceinline__ void xfer_state(const MGState &S, const MGState &V, const StepCaps &c, int lane, int e,
                                            bool in) {
     const int blk = V.N, N = S.N;
 #define XF(f, rows) xfer(V.f, S.f, rows, blk, lane, N, e, in)
+#define XS(f, r) do { if (in) V.f[(uint32_t)(r) * blk + lane] = S.f[(uint32_t)(r) * N + e]; \
+                      else S.f[(uint32_t)(r) * N + e] = V.f[(uint32_t)(r) * blk + lane]; } while (0)
     XF(bpx, c.nb); XF(bpy, c.nb); XF(bvx, c.nb); XF(bvy, c.nb); XF(ba, c.nb); XF(bw, c.nb); XF(bvbx, c.nb);
     XF(bvby, c.nb); XF(bwb, c.nb); XF(brc, c.nb); XF(brs, c.nb); XF(bacache, c.nb);
-    XF(sbbl, c.ns); XF(sbbb, c.ns); XF(sbbr, c.ns); XF(sbbt, c.ns);
-    xfer(V.cp, S.cp, c.nc, blk, lane, N, e, in, CP_NUM, c.nc, MG_MAX_CONS);
-    XF(anx, c.na); XF(any, c.na); XF(au, c.na); XF(akey, c.na); XF(astamp, c.na);
-    XF(astate, c.na); XF(acount, c.na); XF(asa, c.na); XF(asb, c.na); XF(active, c.na);
-    xfer(V.acon, S.acon, c.na, blk, lane, N, e, in, 2 * AC_NUM, c.na, MG_MAX_ARB);
-    xfer(V.ahash, S.ahash, c.na, blk, lane, N, e, in, 2, c.na, MG_MAX_ARB);
-    XF(curr_dt, 1); XF(target_speed, 1); XF(rel_turn, 1); XF(target_finger, 1);
-    XF(nactive, 1); XF(stamp, 1); XF(overflow, 1);
+    // constraint parameter slots: in = MAXF, MAXB, BCOEF, JACC, JACC2, type parameters 8-11; out = JACC, JACC2
+#pragma unroll 1
+    for (int k = 0; k < CP_NUM; k++) {
+        const bool need = in ? (k <= CP_JACC2 || (k >= 8 && k <= 11)) : (k == CP_JACC || k == CP_JACC2);
+        if (!need) continue;
+#pragma unroll 2
+        for (int r = 0; r < c.nc; r++) {
+            const uint32_t li = (uint32_t)(k * c.nc + r) * blk + lane, hi = (uint32_t)(k * MG_MAX_CONS + r) * N + e;
+            if (in) V.cp[li] = S.cp[hi]; else S.cp[hi] = V.cp[li];
+        }
+    }
+#pragma unroll 1
+    for (int r = 0; r < c.na; r++) { // arbiter slots: only live ones carry data
+        XS(akey, r);
+        const int key = in ? V.akey[(uint32_t)r * blk + lane] : V.akey[(uint32_t)r * blk + lane];
+        if (key < 0) continue;
+        XS(anx, r); XS(any, r); XS(au, r); XS(astamp, r); XS(astate, r); XS(acount, r); XS(asa, r); XS(asb, r);
+#pragma unroll 1
+        for (int f = 0; f < 2 * AC_NUM; f++) {
+            if (in) V.acon[(uint32_t)(f * c.na + r) * blk + lane] = S.acon[(uint32_t)(f * MG_MAX_ARB + r) * N + e];
+            else S.acon[(uint32_t)(f * MG_MAX_ARB + r) * N + e] = V.acon[(uint32_t)(f * c.na + r) * blk + lane];
+        }
+        for (int k = 0; k < 2; k++) {
+            if (in) V.ahash[(uint32_t)(k * c.na + r) * blk + lane] = S.ahash[(uint32_t)(k * MG_MAX_ARB + r) * N + e];
+            else S.ahash[(uint32_t)(k * MG_MAX_ARB + r) * N + e] = V.ahash[(uint32_t)(k * c.na + r) * blk + lane];
+        }
+    }
+    XF(nactive, 1);
+    const int nact = V.nactive[lane];
+#pragma unroll 1
+    for (int r = 0; r < nact; r++) XS(active, r);
+    XF(curr_dt, 1); XF(stamp, 1); XF(overflow, 1);
     if (in) { // read-only during the substeps
+        XF(target_speed, 1); XF(rel_turn, 1); XF(target_finger, 1);
         XF(bminv, c.nb); XF(biinv, c.nb);
         XF(sr, c.ns); XF(su, c.ns); XF(sgroup, c.ns); XF(shash, c.ns); XF(sbody, c.ns); XF(spoly, c.ns);
-        XF(ctype, c.nc); XF(ca, c.nc); XF(cb, c.nc);
         XF(nbodies, 1); XF(nshapes, 1); XF(ncons, 1); XF(robot_body0, 1); XF(robot_cons0, 1);
     }
+#undef XS
 #undef XF
 }
 
@@ -127,6 +158,16 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
             if (reset_mask) reset_mask[e] = 0;
             return;
         }
+        bool ok = S.ncons[e] == C.nc && S.robot_body0[e] == 0 && S.robot_cons0[e] == 0;
+        for (int c = 0; c < C.nc; c++) {
+            const ConsDesc d = static_cons(c);
+            ok = ok && AT(S.ctype, c) == d.type && AT(S.ca, c) == d.a && AT(S.cb, c) == d.b;
+        }
+        if (!ok) { // the compiled constraint list does not describe this scene (never expected)
+            S.overflow[e] |= 32;
+            if (reset_mask) reset_mask[e] = 0;
+            return;
+        }
         carve_view(V, smem, C, C.blk);
         xfer_state(S, V, C, lane, e, true);
         ev = lane;
@@ -139,7 +180,7 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
     for (int i = 0; i < 10; i++) {
         robot_update(V, L, ev);
         MG_PP(P, 0);
-        space_step(V, L, ev, dt, P);
+        space_step<LDS ? C.nc : 0>(V, L, ev, dt, P);
     }
     if (LDS) xfer_state(S, V, C, lane, e, false);
     int steps = S.episode_steps[e] + 1;

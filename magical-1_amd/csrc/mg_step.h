@@ -46,10 +46,9 @@ MG_DEV double k_scalar_body(const BodyR &B, V2 r, V2 n) {
 }
 
 // ---- constraints ----------------------------------------------------------
-MG_DEV void cons_prestep(const MGState &S, int e, int c, double dt) {
-    int a = AT(S.ca, c), b = AT(S.cb, c);
+MG_DEV void cons_prestep_impl(const MGState &S, int e, int c, int a, int b, int type, double dt) {
     BodyR A = bodyr(S, e, a), B = bodyr(S, e, b);
-    switch (AT(S.ctype, c)) {
+    switch (type) {
     case MG_C_PIVOT: {
         double ac = a < 0 ? 1.0 : AT(S.brc, a), as = a < 0 ? 0.0 : AT(S.brs, a);
         double bc = AT(S.brc, b), bs = AT(S.brs, b);
@@ -108,10 +107,9 @@ MG_DEV void cons_prestep(const MGState &S, int e, int c, double dt) {
     }
 }
 
-MG_DEV void cons_cached(const MGState &S, int e, int c, double dt_coef) {
-    int a = AT(S.ca, c), b = AT(S.cb, c);
+MG_DEV void cons_cached_impl(const MGState &S, int e, int c, int a, int b, int type, double dt_coef) {
     BodyR A = bodyr(S, e, a), B = bodyr(S, e, b);
-    switch (AT(S.ctype, c)) {
+    switch (type) {
     case MG_C_PIVOT:
         apply_impulses(S, e, A, B, v2(CPA(CP_R1X, c), CPA(CP_R1Y, c)), v2(CPA(CP_R2X, c), CPA(CP_R2Y, c)),
                        vmult(v2(CPA(CP_JACC, c), CPA(CP_JACC2, c)), dt_coef));
@@ -133,10 +131,9 @@ MG_DEV void cons_cached(const MGState &S, int e, int c, double dt_coef) {
     }
 }
 
-MG_DEV void cons_apply(const MGState &S, int e, int c, double dt) {
-    int a = AT(S.ca, c), b = AT(S.cb, c);
+MG_DEV void cons_apply_impl(const MGState &S, int e, int c, int a, int b, int type, double dt) {
     BodyR A = bodyr(S, e, a), B = bodyr(S, e, b);
-    switch (AT(S.ctype, c)) {
+    switch (type) {
     case MG_C_PIVOT: {
         V2 r1 = v2(CPA(CP_R1X, c), CPA(CP_R1Y, c)), r2 = v2(CPA(CP_R2X, c), CPA(CP_R2Y, c));
         V2 vr = relative_velocity(S, e, a, b, r1, r2);
@@ -197,6 +194,51 @@ MG_DEV void cons_apply(const MGState &S, int e, int c, double dt) {
         if (b >= 0) AT(S.bw, b) -= j_damp * B.iinv;
         break;
     }
+    }
+}
+
+MG_DEV void cons_prestep(const MGState &S, int e, int c, double dt) {
+    cons_prestep_impl(S, e, c, AT(S.ca, c), AT(S.cb, c), AT(S.ctype, c), dt);
+}
+MG_DEV void cons_cached(const MGState &S, int e, int c, double dt_coef) {
+    cons_cached_impl(S, e, c, AT(S.ca, c), AT(S.cb, c), AT(S.ctype, c), dt_coef);
+}
+MG_DEV void cons_apply(const MGState &S, int e, int c, double dt) {
+    cons_apply_impl(S, e, c, AT(S.ca, c), AT(S.cb, c), AT(S.ctype, c), dt);
+}
+
+// Constraint lists known at compile time (the LDS step variants): the robot's ten joints in
+// add_robot order (entities.py:238-433) with body slots 0 body, 1 control, 2-3 eyes, 4-5 fingers,
+// then, for one block, its two ground-friction joints (static body -1, block body 6).
+struct ConsDesc { int type, a, b; };
+__host__ __device__ constexpr ConsDesc static_cons(int c) {
+    constexpr ConsDesc T[12] = {{MG_C_PIVOT, 1, 0},   {MG_C_GEAR, 1, 0},     {MG_C_SPRING, 0, 2},  {MG_C_SPRING, 0, 3},
+                                {MG_C_PIVOT, 0, 4},   {MG_C_ROTLIMIT, 0, 4}, {MG_C_MOTOR, 0, 4},   {MG_C_PIVOT, 0, 5},
+                                {MG_C_ROTLIMIT, 0, 5}, {MG_C_MOTOR, 0, 5},   {MG_C_PIVOT, -1, 6},  {MG_C_GEAR, -1, 6}};
+    return T[c];
+}
+template <int NC, int C = 0>
+MG_DEV void static_prestep(const MGState &S, int e, double dt) {
+    if constexpr (C < NC) {
+        constexpr ConsDesc d = static_cons(C);
+        cons_prestep_impl(S, e, C, d.a, d.b, d.type, dt);
+        static_prestep<NC, C + 1>(S, e, dt);
+    }
+}
+template <int NC, int C = 0>
+MG_DEV void static_cached(const MGState &S, int e, double dt_coef) {
+    if constexpr (C < NC) {
+        constexpr ConsDesc d = static_cons(C);
+        cons_cached_impl(S, e, C, d.a, d.b, d.type, dt_coef);
+        static_cached<NC, C + 1>(S, e, dt_coef);
+    }
+}
+template <int NC, int C = 0>
+MG_DEV void static_apply(const MGState &S, int e, double dt) {
+    if constexpr (C < NC) {
+        constexpr ConsDesc d = static_cons(C);
+        cons_apply_impl(S, e, C, d.a, d.b, d.type, dt);
+        static_apply<NC, C + 1>(S, e, dt);
     }
 }
 
@@ -311,6 +353,8 @@ MG_DEV void arbiter_apply(const MGState &S, int e, int slot) {
 }
 
 // ---- cpSpaceStep -----------------------------------------------------------
+// NCS > 0: the constraint list is the compile-time static_cons(0 .. NCS-1) (asserted by the caller)
+template <int NCS = 0>
 MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, MGProf &P) {
     uint32_t stamp = S.stamp[e] + 1;
     S.stamp[e] = stamp;
@@ -331,24 +375,30 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
     MG_PP(P, 1);
     // broadphase + narrowphase, canonical order
     for (int i = 0; i < ns; i++) {
+        // BB tests on the cached BBs; the world-space shape is built only for pairs that pass
+        const double al = AT(S.sbbl, i), ab = AT(S.sbbb, i), ar = AT(S.sbbr, i), at = AT(S.sbbt, i);
         ShapeW A;
-        load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A);
-        int gi = AT(S.sgroup, i), bi = AT(S.sbody, i);
-        double ui = AT(S.su, i);
+        bool have_a = false;
+        const int gi = AT(S.sgroup, i), bi = AT(S.sbody, i);
+        const double ui = AT(S.su, i);
         for (int w = 0; w < 4; w++) {
+            double wl, wb, wr, wt;
+            wall_bb(w, wl, wb, wr, wt);
+            if (!(al <= wr && wl <= ar && ab <= wt && wb <= at)) continue;
+            if (!have_a) { load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A); have_a = true; }
             ShapeW W;
             load_wall(w, W);
-            if (!bb_intersects(A, W)) continue;
             Collision info;
             collide(A, W, info);
             if (info.count) arbiter_update(S, L, e, i * 128 + 100 + w, A, W, ui, 0.8, info);
         }
         for (int j = i + 1; j < ns; j++) {
-            if (!(A.bbl <= AT(S.sbbr, j) && AT(S.sbbl, j) <= A.bbr && A.bbb <= AT(S.sbbt, j) && AT(S.sbbb, j) <= A.bbt))
+            if (!(al <= AT(S.sbbr, j) && AT(S.sbbl, j) <= ar && ab <= AT(S.sbbt, j) && AT(S.sbbb, j) <= at))
                 continue;
             if (AT(S.sbody, j) == bi) continue;
             int gj = AT(S.sgroup, j);
             if (gi != 0 && gi == gj) continue;
+            if (!have_a) { load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A); have_a = true; }
             ShapeW B;
             load_shape(S, L, e, j, (uint64_t)AT(S.shash, j), B);
             Collision info;
@@ -368,16 +418,19 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
     nact = S.nactive[e];
     int nc = S.ncons[e];
     for (int i = 0; i < nact; i++) arbiter_prestep(S, L, e, AT(S.active, i), dt);
-    for (int c = 0; c < nc; c++) cons_prestep(S, e, c, dt);
+    if constexpr (NCS > 0) static_prestep<NCS>(S, e, dt);
+    else for (int c = 0; c < nc; c++) cons_prestep(S, e, c, dt);
     MG_PP(P, 4);
     // velocity integration is the identity here (no gravity, damping 1, no forces)
     double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
     for (int i = 0; i < nact; i++) arbiter_cached(S, e, AT(S.active, i), dt_coef);
-    for (int c = 0; c < nc; c++) cons_cached(S, e, c, dt_coef);
+    if constexpr (NCS > 0) static_cached<NCS>(S, e, dt_coef);
+    else for (int c = 0; c < nc; c++) cons_cached(S, e, c, dt_coef);
     MG_PP(P, 5);
     for (int it = 0; it < 10; it++) {
         for (int i = 0; i < nact; i++) arbiter_apply(S, e, AT(S.active, i));
-        for (int c = 0; c < nc; c++) cons_apply(S, e, c, dt);
+        if constexpr (NCS > 0) static_apply<NCS>(S, e, dt);
+        else for (int c = 0; c < nc; c++) cons_apply(S, e, c, dt);
     }
     MG_PP(P, 6);
 }
