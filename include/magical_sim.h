@@ -78,6 +78,9 @@ int mg_seed(mg_sim *sim, const uint32_t *seeds_host);
 /* device-side uniform random actions for throughput runs (Philox 4x32-10, key, counter = (step, env)) */
 int mg_random_actions(mg_sim *sim, uint8_t *actions_dev, uint64_t key, uint64_t step, void *stream);
 int mg_num_envs(const mg_sim *sim);
+/* self-test of the device's correctly rounded sin/cos (the physics and render transforms use it):
+ * device f64 x[n] -> sin, cos */
+int mg_selftest_sincos(const double *x_dev, double *sin_dev, double *cos_dev, int n, void *stream);
 /* per-kernel timing of the next max_steps mg_step calls (hipEvents on the launch stream); 0 disables */
 int mg_enable_timing(mg_sim *sim, int max_steps);
 /* out[0] = total ms in the physics/step kernel, out[1] = total ms in the render kernel,

@@ -95,11 +95,54 @@ MG_DEV dd_t mg_kcos(dd_t r) {
     return p;
 }
 
-// correctly rounded (cos x, sin x)
-MG_DEV void mg_sincos(double x, double &s, double &c) {
-    if (fabs(x) < 7.450580596923828e-09) { s = x; c = 1.0; return; }
-    int q; dd_t r;
-    mg_reduce_pio2(x, q, r);
+// Ziv-style fast path: sin(r), cos(r) for the reduced r = rh + rl with the leading terms in
+// double-double and the tail r^7.. / r^8.. in double (absolute error < 2^-66 |result|), then a
+// rounding test: the double nearest to the double-double is returned only when the exact value
+// provably rounds to it; otherwise the caller falls back to the full double-double series.  Both
+// paths therefore return the correctly rounded value (as the oracle does).
+MG_DEV double mg_ifh(int n) { return MG_INVF_HI[n]; }
+MG_DEV dd_t mg_ifd(int n) { return {MG_INVF_HI[n], MG_INVF_LO[n]}; }
+
+MG_DEV bool mg_certify(dd_t y, double &out) {
+    y = dd_fast_two_sum(y.hi, y.lo);
+    const uint64_t bits = (uint64_t)__double_as_longlong(y.hi);
+    const int ex = (int)((bits >> 52) & 0x7FF);
+    if (ex < 64 || (bits & 0xFFFFFFFFFFFFFull) == 0) return false; // tiny, or a power of two (ulp changes)
+    const double half_ulp = __longlong_as_double((long long)((uint64_t)(ex - 53) << 52));
+    const double eps = fabs(y.hi) * 2.168404344971009e-19;          // 2^-62 |y| (error bound 2^-65)
+    if (fabs(y.lo) + eps < half_ulp) { out = y.hi; return true; }
+    return false;
+}
+
+MG_DEV bool mg_fast_sin(dd_t r, double &out) {
+    const dd_t r2 = dd_mul(r, r);
+    const double t = r2.hi;
+    double p = mg_ifh(21);
+    p = __fma_rn(p, t, -mg_ifh(19)); p = __fma_rn(p, t, mg_ifh(17)); p = __fma_rn(p, t, -mg_ifh(15));
+    p = __fma_rn(p, t, mg_ifh(13));  p = __fma_rn(p, t, -mg_ifh(11)); p = __fma_rn(p, t, mg_ifh(9));
+    p = __fma_rn(p, t, -mg_ifh(7));                                    // T7 = sum_{k>=3} (-1)^k t^(k-3) / (2k+1)!
+    dd_t q = dd_add(mg_ifd(5), {t * p, 0.0});                          // 1/5! + r^2 T7
+    q = dd_add(dd_neg(mg_ifd(3)), dd_mul(r2, q));                      // -1/3! + r^2 (...)
+    q = dd_add({1.0, 0.0}, dd_mul(r2, q));
+    return mg_certify(dd_mul(r, q), out);
+}
+
+MG_DEV bool mg_fast_cos(dd_t r, double &out) {
+    const dd_t r2 = dd_mul(r, r);
+    const double t = r2.hi;
+    double p = -mg_ifh(22);
+    p = __fma_rn(p, t, mg_ifh(20)); p = __fma_rn(p, t, -mg_ifh(18)); p = __fma_rn(p, t, mg_ifh(16));
+    p = __fma_rn(p, t, -mg_ifh(14)); p = __fma_rn(p, t, mg_ifh(12)); p = __fma_rn(p, t, -mg_ifh(10));
+    p = __fma_rn(p, t, mg_ifh(8));                                     // T8 = sum_{k>=4} (-1)^k t^(k-4) / (2k)!
+    dd_t q = dd_add(dd_neg(mg_ifd(6)), {t * p, 0.0});                  // -1/6! + r^2 T8
+    q = dd_add(mg_ifd(4), dd_mul(r2, q));
+    q = dd_add(dd_neg(mg_ifd(2)), dd_mul(r2, q));
+    return mg_certify(dd_add({1.0, 0.0}, dd_mul(r2, q)), out);
+}
+
+// full double-double series: the rare arguments the fast path cannot certify (kept out of line)
+__device__ __noinline__ void mg_sincos_slow(double rh, double rl, int q, double *s, double *c) {
+    dd_t r = {rh, rl};
     dd_t ks = mg_ksin(r), kc = mg_kcos(r), vs, vc;
     switch (q) {
     case 0: vs = ks; vc = kc; break;
@@ -107,8 +150,31 @@ MG_DEV void mg_sincos(double x, double &s, double &c) {
     case 2: vs = dd_neg(ks); vc = dd_neg(kc); break;
     default: vs = dd_neg(kc); vc = ks; break;
     }
-    s = vs.hi + vs.lo;
-    c = vc.hi + vc.lo;
+    *s = vs.hi + vs.lo;
+    *c = vc.hi + vc.lo;
+}
+
+// correctly rounded (cos x, sin x)
+MG_DEV void mg_sincos(double x, double &s, double &c) {
+    if (fabs(x) < 7.450580596923828e-09) { s = x; c = 1.0; return; }
+    int q; dd_t r;
+    mg_reduce_pio2(x, q, r);
+    double fs, fc;
+    const bool ok_s = mg_fast_sin(r, fs), ok_c = mg_fast_cos(r, fc);
+    if (ok_s && ok_c) {
+        double vs, vc;
+        switch (q) {
+        case 0: vs = fs; vc = fc; break;
+        case 1: vs = fc; vc = -fs; break;
+        case 2: vs = -fs; vc = -fc; break;
+        default: vs = -fc; vc = fs; break;
+        }
+        s = vs; c = vc;
+    } else {
+        double ss, cc;
+        mg_sincos_slow(r.hi, r.lo, q, &ss, &cc);
+        s = ss; c = cc;
+    }
     if (fabs(x) < 1.4901161193847656e-08) s = x; // |x| < 2^-26: sin rounds to x
 }
 

@@ -70,6 +70,13 @@ __global__ void __launch_bounds__(64) errors_kernel(MGState S, int32_t *out) {
     out[e] = S.overflow[e];
 }
 
+// self-test of the device correctly rounded sincos (tests/test_gpu_parity.py compares with the oracle)
+__global__ void __launch_bounds__(256) sincos_kernel(const double *x, double *s, double *c, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    mg_sincos(x[i], s[i], c[i]);
+}
+
 // Philox4x32-10 (Salmon et al. 2011): counter = (step lo, step hi, env, 0), key = (k lo, k hi)
 __device__ __forceinline__ uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t &hi) {
     uint64_t p = (uint64_t)a * b;
@@ -321,6 +328,14 @@ int mg_get_bodies(mg_sim *s, double *out, int32_t *counts, void *stream) {
     if (!s || !out) return set_err(-22, "mg_get_bodies: null argument");
     HIPC(hipSetDevice(s->device));
     hipLaunchKernelGGL(bodies_kernel, dim3(grid64(s)), dim3(64), 0, as_stream(stream), s->S, out, counts);
+    HIPC(hipGetLastError());
+    return 0;
+}
+
+int mg_selftest_sincos(const double *x, double *s_out, double *c_out, int n, void *stream) {
+    if (!x || !s_out || !c_out || n < 0) return set_err(-22, "mg_selftest_sincos: bad argument");
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(sincos_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), x, s_out, c_out, n);
     HIPC(hipGetLastError());
     return 0;
 }

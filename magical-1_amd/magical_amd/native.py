@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(HERE, "libmagical_sim_prof.so" if os.environ.get("MAGICA
 
 EXPORTS = ["mg_create", "mg_bind_outputs", "mg_reset", "mg_step", "mg_render_full", "mg_get_bodies",
            "mg_get_errors", "mg_seed", "mg_random_actions", "mg_num_envs", "mg_enable_timing", "mg_read_timing",
-           "mg_destroy", "mg_last_error"]
+           "mg_selftest_sincos", "mg_destroy", "mg_last_error"]
 
 
 class mg_config(ctypes.Structure):
@@ -55,6 +55,7 @@ def load():
     lib.mg_seed.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
     lib.mg_random_actions.argtypes = [vp, vp, u64, u64, vp]
     lib.mg_num_envs.argtypes = [vp]
+    lib.mg_selftest_sincos.argtypes = [vp, vp, vp, i32, vp]
     lib.mg_enable_timing.argtypes = [vp, i32]
     lib.mg_read_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
     lib.mg_destroy.argtypes = [vp]

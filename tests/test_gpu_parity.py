@@ -136,3 +136,27 @@ def test_full_size_sampled_parity(name, n, steps):
                 assert np.array_equal(got[k][j], ref[k]), f"step {t} env {i} obs {k}"
     assert int(vec.errors().abs().sum().item()) == 0
     vec.close()
+
+
+@pytest.mark.gpu
+def test_device_sincos_is_correctly_rounded():
+    """The device sin/cos (fast certified path + double-double fallback) equals the oracle's
+    correctly rounded sin/cos on 1M arguments, incl. arguments next to multiples of pi/2."""
+    import ctypes
+    from magical_amd import native
+    lib = native.load()
+    rs = np.random.RandomState(123)
+    x = np.concatenate([rs.uniform(-8, 8, 400000), rs.uniform(-1e-3, 1e-3, 100000),
+                        rs.uniform(-40, 40, 400000),
+                        (np.arange(-50, 51)[:, None] * (np.pi / 2) + rs.uniform(-1e-9, 1e-9, (101, 990))).ravel()])
+    xd = torch.as_tensor(x, dtype=torch.float64, device="cuda")
+    s = torch.empty_like(xd)
+    c = torch.empty_like(xd)
+    native.check(lib.mg_selftest_sincos(ctypes.c_void_p(xd.data_ptr()), ctypes.c_void_p(s.data_ptr()),
+                                        ctypes.c_void_p(c.data_ptr()), len(x), None))
+    torch.cuda.synchronize()
+    s, c = s.cpu().numpy(), c.cpu().numpy()
+    L = po.lib()
+    ref_s = np.array([L.o_crsin(float(v)) for v in x])
+    ref_c = np.array([L.o_crcos(float(v)) for v in x])
+    assert np.array_equal(s, ref_s) and np.array_equal(c, ref_c)
