@@ -57,9 +57,9 @@ def main():
         fetch = write = None
         for db in glob.glob(os.path.join(a.dir, "**", "*.db"), recursive=True):
             for k, cn, n, avg, _ in pmc(db):
-                if k == a.kernel and cn == "FETCH_SIZE":
+                if k.startswith(a.kernel) and cn == "FETCH_SIZE":
                     fetch = avg * 1024 * 2
-                if k == a.kernel and cn == "WRITE_SIZE":
+                if k.startswith(a.kernel) and cn == "WRITE_SIZE":
                     write = avg * 1024
         data = {}
         if os.path.exists(a.traffic_json):
