@@ -61,7 +61,8 @@ struct RenderSmem {
             int32_t lkr[RG_MAXLONG][3];     // klo, khi, ordinal
         } post;
     } u;
-    uint4 ginfo[RG_MAXG];                     // (ymin|ymax<<16, xmin|xmax<<16, top|bot<<16, v0|n<<16)
+    uint4 ginfo[RG_MAXG];                     // (ymin|ymax<<16, xmin|xmax<<16, -, -); int32 atomics while built
+    int32_t gchg[RG_MAXG];                    // direction changes of the y sequence around each polygon
     uint32_t bspan[RG_MAXG][RG_BAND];         // spans of the band's rows, per band-list slot: l | r << 16
     uint64_t col[2 * RG_MAXG + 2];            // R | G << 16 | B << 32 per ordinal
     int16_t g_rpoly[RG_MAXG], g_voff[RG_MAXG + 1], g_nv[RG_MAXG];
@@ -465,26 +466,38 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         }
     }
     RG_SYNC();
-    // ---- 4. per-geom bounds and chains (top / bottom vertex; both chains must be y-monotone);
-    //         outline items per band ----
+    // ---- 4. per-geom bounds (vertex-parallel atomics) and the convexity premise of the fill: going
+    //         round a polygon the sign of dy changes exactly twice (both vertex chains y-monotone) ----
     for (int g = tid; g < G; g += RG_THREADS) {
-        const int v0 = sm.g_voff[g], n = sm.g_nv[g];
-        int ymin = sm.vy[v0], ymax = ymin, xmin = sm.vx[v0], xmax = xmin, top = 0, bot = 0;
-        for (int i = 1; i < n; i++) {
-            int y = sm.vy[v0 + i], x = sm.vx[v0 + i];
-            if (y < ymin) { ymin = y; top = i; }
-            if (y > ymax) { ymax = y; bot = i; }
-            xmin = x < xmin ? x : xmin; xmax = x > xmax ? x : xmax;
+        int32_t *b = (int32_t *)&sm.ginfo[g];
+        b[0] = 32767; b[1] = -32768; b[2] = 32767; b[3] = -32768;
+        sm.gchg[g] = 0;
+    }
+    RG_SYNC();
+    for (int v = tid; v < NV; v += RG_THREADS) {
+        const int g = sm.v_geom[v], v0 = sm.g_voff[g], n = sm.g_nv[g];
+        int32_t *b = (int32_t *)&sm.ginfo[g];
+        const int x = sm.vx[v], y = sm.vy[v];
+        atomicMin(&b[0], y); atomicMax(&b[1], y); atomicMin(&b[2], x); atomicMax(&b[3], x);
+        const int nx = v + 1 == v0 + n ? v0 : v + 1;
+        const int d = sm.vy[nx] - y;
+        if (d == 0) continue;
+        int p = v, dp = 0;
+        for (int k = 0; k < n && dp == 0; k++) { // previous edge with dy != 0
+            const int pp = p == v0 ? v0 + n - 1 : p - 1;
+            dp = sm.vy[p] - sm.vy[pp];
+            p = pp;
         }
-        bool mono = true;
-        for (int i = top, py = ymin; i != bot; ) { i = i + 1 == n ? 0 : i + 1; int y = sm.vy[v0 + i]; mono &= y >= py; py = y; }
-        for (int i = top, py = ymin; i != bot; ) { i = i == 0 ? n - 1 : i - 1; int y = sm.vy[v0 + i]; mono &= y >= py; py = y; }
-        if (!mono) sm.err = 4;
-        xmin = xmin > 0 ? xmin : 0;
-        xmax = xmax < MG_RES - 1 ? xmax : MG_RES - 1;
+        if ((dp > 0) != (d > 0)) atomicAdd(&sm.gchg[g], 1);
+    }
+    RG_SYNC();
+    for (int g = tid; g < G; g += RG_THREADS) {
+        const int32_t *b = (const int32_t *)&sm.ginfo[g];
+        const int ymin = b[0], ymax = b[1];
+        const int xmin = b[2] > 0 ? b[2] : 0, xmax = b[3] < MG_RES - 1 ? b[3] : MG_RES - 1;
+        if (sm.gchg[g] != 2 && sm.gchg[g] != 0) sm.err = 4;
         sm.ginfo[g] = make_uint4((uint32_t)(uint16_t)ymin | ((uint32_t)(uint16_t)ymax << 16),
-                                 (uint32_t)(uint16_t)xmin | ((uint32_t)(uint16_t)xmax << 16),
-                                 (uint32_t)top | ((uint32_t)bot << 16), (uint32_t)v0 | ((uint32_t)n << 16));
+                                 (uint32_t)(uint16_t)xmin | ((uint32_t)(uint16_t)xmax << 16), 0u, 0u);
     }
     if (sm.ndash > SM::RG_MAXDASH) sm.err = 1;
     const int nitems = sm.nsedge + (sm.ndash < SM::RG_MAXDASH ? sm.ndash : SM::RG_MAXDASH);
@@ -538,6 +551,9 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     }
     const int nsedge = sm.nsedge;
     MG_PROF(0);
+#ifdef MG_PROFILE
+    if (out.debug_skip & 16) return;  // setup only
+#endif
     // ---- 5. bands ----
     uint8_t *ring = view == 0 ? S.hist_allo : S.hist_ego;
     const size_t FR = (size_t)MG_LORES * MG_LORES * 3;
@@ -727,24 +743,28 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         if (plain && !(dskip & 4))
             for (int c = tid; c < RG_BANDLO16; c += RG_THREADS)
                 *(uint4 *)(o_plain + (size_t)e * FR + lrow + 16 * c) = sm.u.post.lo[c];
-        if (stacked && !(dskip & 4)) {
-            // FlattenFrameStack: [96][96][12] = frames oldest..newest concatenated per pixel
-            const uint8_t *p8 = (const uint8_t *)sm.u.post.past;
-            for (int c = tid; c < 4 * RG_BANDLO16; c += RG_THREADS) {
-                uint8_t b[16];
+        if (stacked && !(dskip & 4) && tid < 2 * MG_LORES / 4) {
+            // FlattenFrameStack: [96][96][12] = frames oldest..newest concatenated per pixel; one thread
+            // per 4 pixels: 3 dwords of each frame in, 12 dwords (3 x 16 B) out
+            const uint32_t *p32 = (const uint32_t *)sm.u.post.past, *c32 = (const uint32_t *)sm.u.post.lo;
+            uint32_t f[4][3];
 #pragma unroll
-                for (int j = 0; j < 16; j++) {
-                    int byte = 16 * c + j, px = byte / 12, k = (byte % 12) / 3, ch = byte % 3;
-                    int src = px * 3 + ch;
-                    b[j] = (k == 3 || fresh) ? lo8[src] : p8[k * RG_BANDLO + src];
-                }
-                uint4 w;
-                w.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
-                w.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
-                w.z = b[8] | (b[9] << 8) | (b[10] << 16) | ((uint32_t)b[11] << 24);
-                w.w = b[12] | (b[13] << 8) | (b[14] << 16) | ((uint32_t)b[15] << 24);
-                *(uint4 *)(o_stack + (size_t)e * FR * 4 + lrow * 4 + 16 * c) = w;
+            for (int w = 0; w < 3; w++) {
+                f[3][w] = c32[3 * tid + w];
+#pragma unroll
+                for (int k = 0; k < 3; k++) f[k][w] = fresh ? f[3][w] : p32[k * (RG_BANDLO / 4) + 3 * tid + w];
             }
+            uint32_t o[12];
+#pragma unroll
+            for (int b = 0; b < 48; b++) {   // output byte b: pixel b / 12, frame (b % 12) / 3, channel b % 3
+                const int px = b / 12, k = (b % 12) / 3, sb = 3 * px + b % 3;  // source byte within 12
+                const uint32_t byte = (f[k][sb / 4] >> (8 * (sb % 4))) & 255u;
+                if (b % 4 == 0) o[b / 4] = byte; else o[b / 4] |= byte << (8 * (b % 4));
+            }
+            uint4 *dst = (uint4 *)(o_stack + (size_t)e * FR * 4 + lrow * 4) + 3 * tid;
+            dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+            dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+            dst[2] = make_uint4(o[8], o[9], o[10], o[11]);
         }
         RG_SYNC();
         MG_PROF(4);
