@@ -28,6 +28,8 @@ hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, in
                           const uint8_t *actions, float *reward, uint8_t *done, double *eval_score, uint8_t *reset_mask,
                           hipStream_t st);
 hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderOut &ro, int mode, hipStream_t st);
+hipError_t mg_launch_compose3ea(const MGState &S, const uint8_t *obs_allo, const uint8_t *mask, uint8_t *obs_past,
+                                hipStream_t st);
 // profiling builds (-DMG_PROFILE): copy and clear each translation unit's phase timers
 hipError_t mg_prof_read_physics(unsigned long long *out64);
 hipError_t mg_prof_read_raster(unsigned long long *out64);

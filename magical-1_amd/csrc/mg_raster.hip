@@ -10,6 +10,48 @@ hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderO
     return hipGetLastError();
 }
 
+// LoRes3EA (benchmarks/__init__.py lores_ea_entry_point: FlattenFrameStack with allo depth 1, ego
+// depth 3): past_obs[y][x] = allo_t | ego_t-2 | ego_t-1 | ego_t (12 bytes per pixel). The two views are
+// rendered by different workgroups, so this small pass runs after the render kernel and interleaves the
+// current allo frame (obs_allo) with the ego ring (slot nh = t, nh-1, nh-2; all slots equal after reset).
+// One thread per 4 pixels: 4 x 3 dwords in, 3 x 16 B out.
+__global__ __launch_bounds__(256) void compose3ea_kernel(MGState S, const uint8_t *obs_allo, const uint8_t *mask,
+                                                         uint8_t *obs_past) {
+    constexpr int Q = MG_LORES * MG_LORES / 4;   // pixel quads per frame
+    const size_t FR = (size_t)MG_LORES * MG_LORES * 3;
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int e = (int)(gid / Q), q = (int)(gid % Q);
+    if (e >= S.n_envs || (mask && !mask[e])) return;
+    const int nh = S.hist_head[S.N + e];
+    const uint32_t *src[4];
+    src[0] = (const uint32_t *)(obs_allo + (size_t)e * FR);
+    for (int k = 1; k < 4; k++) src[k] = (const uint32_t *)(S.hist_ego + ((size_t)((nh + k + 1) & 3) * S.N + e) * FR);
+    uint32_t f[4][3];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int w = 0; w < 3; w++) f[k][w] = src[k][3 * q + w];
+    uint32_t o[12];
+#pragma unroll
+    for (int b = 0; b < 48; b++) {   // output byte b: pixel b / 12, source (b % 12) / 3, channel b % 3
+        const int px = b / 12, k = (b % 12) / 3, sb = 3 * px + b % 3;
+        const uint32_t byte = (f[k][sb / 4] >> (8 * (sb % 4))) & 255u;
+        if (b % 4 == 0) o[b / 4] = byte; else o[b / 4] |= byte << (8 * (b % 4));
+    }
+    uint4 *dst = (uint4 *)(obs_past + (size_t)e * FR * 4) + 3 * q;
+    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+    dst[2] = make_uint4(o[8], o[9], o[10], o[11]);
+}
+
+hipError_t mg_launch_compose3ea(const MGState &S, const uint8_t *obs_allo, const uint8_t *mask, uint8_t *obs_past,
+                                hipStream_t st) {
+    const int64_t n = (int64_t)S.n_envs * (MG_LORES * MG_LORES / 4);
+    hipLaunchKernelGGL(compose3ea_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, S, obs_allo, mask,
+                       obs_past);
+    return hipGetLastError();
+}
+
 hipError_t mg_prof_read_raster(unsigned long long *out) {
 #ifdef MG_PROFILE
     unsigned long long v[64], z[64] = {0};

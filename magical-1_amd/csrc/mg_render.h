@@ -564,6 +564,8 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     const bool stacked = pp == MG_PREPROC_LORESSTACK || (pp == MG_PREPROC_LORES4E && view == 1) ||
                          (pp == MG_PREPROC_LORES4A && view == 0);
     const bool plain = pp != MG_PREPROC_LORESSTACK;   // the view's own current-frame output
+    // frame ring kept only where a stack reads it (LoRes3EA: ego ring, read by compose3ea_kernel)
+    const bool keep_ring = stacked || (pp == MG_PREPROC_LORES3EA && view == 1);
     uint8_t *o_plain = view == 0 ? out.obs_allo : out.obs_ego;
     uint8_t *o_stack = pp == MG_PREPROC_LORESSTACK ? o_plain : out.obs_past;
     const int oyl = tid / MG_LORES, ox = tid % MG_LORES, x0 = 4 * ox;
@@ -736,7 +738,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         for (int i = tid; i < nbl * RG_BAND; i += RG_THREADS)  // band spans back to empty for the next band
             (&sm.bspan[0][0])[i] = (uint32_t)RG_EMPTY | ((uint32_t)RG_EMPTY << 16);
         // ring of the last 4 LoRes frames: slot nh (all 4 slots at episode start)
-        for (int t = tid; t < (fresh ? 4 : 1) * RG_BANDLO16 && !(dskip & 4); t += RG_THREADS) {
+        for (int t = tid; keep_ring && t < (fresh ? 4 : 1) * RG_BANDLO16 && !(dskip & 4); t += RG_THREADS) {
             int sl = fresh ? t / RG_BANDLO16 : nh, c = t % RG_BANDLO16;
             *(uint4 *)(ring + ((size_t)sl * S.N + e) * FR + lrow + 16 * c) = sm.u.post.lo[c];
         }

@@ -195,6 +195,8 @@ static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
     ro.obs_allo = s->out.obs_allo; ro.obs_ego = s->out.obs_ego; ro.obs_past = s->out.obs_past;
     ro.preproc = s->preproc;
     HIPC(mg_launch_render(s->S, s->dlib, ro, 0, st));
+    if (s->preproc == MG_PREPROC_LORES3EA)
+        HIPC(mg_launch_compose3ea(s->S, (const uint8_t *)s->out.obs_allo, mask, (uint8_t *)s->out.obs_past, st));
     return 0;
 }
 
@@ -222,7 +224,7 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     if (cfg->num_envs <= 0) return set_err(-22, "mg_create: num_envs must be positive");
     if (cfg->task < 0 || cfg->task > 4) return set_err(-22, "mg_create: unknown task");
     if (cfg->preproc != MG_PREPROC_LORES4E && cfg->preproc != MG_PREPROC_LORESSTACK &&
-        cfg->preproc != MG_PREPROC_LORES4A && cfg->preproc != MG_PREPROC_NONE)
+        cfg->preproc != MG_PREPROC_LORES4A && cfg->preproc != MG_PREPROC_LORES3EA && cfg->preproc != MG_PREPROC_NONE)
         return set_err(-95, "mg_create: preprocessor not supported by the GPU path");
     HIPC(hipSetDevice(cfg->device));
     mg_sim *s = new mg_sim();
@@ -272,7 +274,8 @@ int mg_bind_outputs(mg_sim *s, const mg_buffers *b) {
     if (!s || !b) return set_err(-22, "mg_bind_outputs: null argument");
     if (s->preproc != MG_PREPROC_NONE && (!b->obs_allo || !b->obs_ego))
         return set_err(-22, "mg_bind_outputs: obs_allo / obs_ego required");
-    if ((s->preproc == MG_PREPROC_LORES4E || s->preproc == MG_PREPROC_LORES4A) && !b->obs_past)
+    if ((s->preproc == MG_PREPROC_LORES4E || s->preproc == MG_PREPROC_LORES4A || s->preproc == MG_PREPROC_LORES3EA) &&
+        !b->obs_past)
         return set_err(-22, "mg_bind_outputs: obs_past required for this preprocessor");
     const void *ptrs[3] = {b->obs_allo, b->obs_ego, b->obs_past};
     for (const void *p : ptrs)

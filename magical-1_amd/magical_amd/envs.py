@@ -55,13 +55,11 @@ class VecMagicalEnv:
         if not self.spec.gpu_supported:
             raise NotImplementedError(f"{env_name}: task not on the GPU hot path yet")
         pp = self.spec.preproc
-        if pp in ("LoRes3EA",):
-            raise NotImplementedError(f"{env_name}: preprocessor {pp} not implemented on the GPU path yet")
         self.num_envs = int(num_envs)
         self.device = torch.device(device)
         self.lib = native.load()
         self._chw = pp is not None and registry.PREPROCESSORS[pp].get("channels_first", False)
-        gpu_pp = {None: 0, "LoRes4E": 1, "LoResStack": 2, "LoRes4A": 4, "LoResCHW4E": 1, "LoResCHW4A": 1}[pp]
+        gpu_pp = {None: 0, "LoRes4E": 1, "LoResStack": 2, "LoRes3EA": 3, "LoRes4A": 4, "LoResCHW4E": 1, "LoResCHW4A": 1}[pp]
         cfg = native.mg_config()
         cfg.task = self.spec.task_id
         cfg.rand_flags = self.spec.rand_flags

@@ -20,6 +20,14 @@ CONFIGS = [
     ("ClusterColour-Demo-LoResStack-v0", 3, 60),
     ("MatchRegions-TestAll-LoRes4E-v0", 4, 130),
 ]
+# the other observation preprocessors (benchmarks/__init__.py:51-190): same rollout check
+PREPROC_CONFIGS = [
+    ("MoveToRegion-Demo-LoRes3EA-v0", 4, 45),
+    ("MoveToCorner-TestAll-LoRes4A-v0", 3, 30),
+    ("MoveToRegion-TestAll-LoResCHW4E-v0", 3, 30),
+    ("MoveToRegion-Demo-LoResCHW4A-v0", 2, 12),
+    ("MoveToRegion-TestJitter-v0", 2, 12),
+]
 POSE_TOL = 1e-9
 
 
@@ -38,7 +46,7 @@ def oracle_env(spec, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,n,steps", CONFIGS)
+@pytest.mark.parametrize("name,n,steps", CONFIGS + PREPROC_CONFIGS)
 def test_rollout_parity(name, n, steps):
     spec = registry.lookup(name)
     seeds = [1000 + i for i in range(n)]
@@ -160,3 +168,37 @@ def test_device_sincos_is_correctly_rounded():
     ref_s = np.array([L.o_crsin(float(v)) for v in x])
     ref_c = np.array([L.o_crcos(float(v)) for v in x])
     assert np.array_equal(s, ref_s) and np.array_equal(c, ref_c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["MoveToRegion-Demo-LoRes3EA-v0", "MoveToRegion-Demo-LoRes4E-v0"])
+def test_masked_reset(name):
+    """reset(mask) resets exactly the masked envs (SB3 VecEnv per-env reset); the
+    others keep their state, frame stacks and observations."""
+    spec = registry.lookup(name)
+    n = 6
+    seeds = [50 + i for i in range(n)]
+    vec = magical_amd.make_vec(name, n, seeds=seeds, auto_reset=False)
+    orc = [oracle_env(spec, s) for s in seeds]
+    vec.reset()
+    for o in orc:
+        o.reset()
+    acts = np.random.RandomState(5).randint(0, 18, (12, n))
+    mask = np.array([1, 0, 0, 1, 0, 1], dtype=np.uint8)
+    for t in range(12):
+        if t == 6:
+            obs = vec.reset(torch.as_tensor(mask))
+            got = {k: v.cpu().numpy() for k, v in obs.items()}
+            for i in range(n):
+                if mask[i]:
+                    ref = oracle_obs_split(spec, orc[i].reset())
+                    for k in got:
+                        assert np.array_equal(got[k][i], ref[k]), f"masked reset env {i} obs {k}"
+        obs, rew, done, info = vec.step(torch.as_tensor(acts[t], dtype=torch.uint8))
+        got = {k: v.cpu().numpy() for k, v in obs.items()}
+        for i in range(n):
+            o, r, d, s = orc[i].step(int(acts[t, i]))
+            ref = oracle_obs_split(spec, o)
+            for k in got:
+                assert np.array_equal(got[k][i], ref[k]), f"step {t} env {i} obs {k}"
+    vec.close()
