@@ -569,48 +569,53 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     uint8_t *o_plain = view == 0 ? out.obs_allo : out.obs_ego;
     uint8_t *o_stack = pp == MG_PREPROC_LORESSTACK ? o_plain : out.obs_past;
     const int oyl = tid / MG_LORES, ox = tid % MG_LORES, x0 = 4 * ox;
+    const bool do_pf = mode == 0 && stacked && !fresh && tid < 3 * RG_BANDLO16;
+#ifdef MG_PROFILE
+    const int dskip = out.debug_skip;
+#else
+    const int dskip = 0;
+#endif
+    // prefetch frames t-3..t-1 of band y0's rows (ring slots nh+1..nh+3, never written this step)
+    auto prefetch = [&](int y0) {
+        int k = tid / RG_BANDLO16, c = tid % RG_BANDLO16, sl = (nh + 1 + k) & 3;
+        return *(const uint4 *)(ring + ((size_t)sl * S.N + e) * FR + (size_t)(y0 / 4) * RG_LOROW + 16 * c);
+    };
+    // geoms whose rows meet band y0, in draw order (ballot compaction by one wave)
+    auto band_list = [&](int y0) {
+        int cnt = 0;
+        for (int base = 0; base < G; base += 64) {
+            const int g = base + lane;
+            bool ov = false;
+            if (g < G) {
+                const uint4 gi = sm.ginfo[g];
+                const int ymin = (int16_t)(gi.x & 0xFFFF), ymax = (int16_t)(gi.x >> 16);
+                const int xmin = (int16_t)(gi.y & 0xFFFF), xmax = (int16_t)(gi.y >> 16);
+                ov = ymax >= y0 && ymin < y0 + RG_BAND && xmin <= xmax;
+            }
+            const uint64_t m = __ballot(ov);
+            if (ov) {
+                const int slot = cnt + __popcll(m & ((1ull << lane) - 1ull));
+                sm.blist[slot] = (int16_t)g;
+                sm.gslot[g] = (int16_t)slot;
+            }
+            cnt += __popcll(m);
+        }
+        if (lane == 0) sm.nblist = cnt;
+    };
+    // band 0 prologue: outline layer cleared, band list, prefetch (later bands: in the previous band's tail)
+    uint4 pf = make_uint4(0, 0, 0, 0);
+    if (do_pf) pf = prefetch(0);
+    for (int i = tid; i < RG_BAND * MG_RES / 4; i += RG_THREADS)
+        ((uint4 *)&sm.u.post.band[0][0])[i] = make_uint4(0, 0, 0, 0);
+    if (tid == 0) sm.nlong = 0;
+    if (tid >= 128) band_list(0);
+#ifdef MG_PROFILE
+    if (tid < 4) sm.pw[tid] = 0u;
+#endif
+    RG_SYNC();
     for (int y0 = 0, band_i = 0; y0 < MG_RES; y0 += RG_BAND, band_i++) {
         const size_t lrow = (size_t)(y0 / 4) * RG_LOROW;  // byte offset of this band's LoRes rows
-        // prefetch frames t-3..t-1 of these rows (ring slots nh+1..nh+3, never written this step)
-        uint4 pf = make_uint4(0, 0, 0, 0);
-        const bool do_pf = mode == 0 && stacked && !fresh && tid < 3 * RG_BANDLO16;
-        if (do_pf) {
-            int k = tid / RG_BANDLO16, c = tid % RG_BANDLO16, sl = (nh + 1 + k) & 3;
-            pf = *(const uint4 *)(ring + ((size_t)sl * S.N + e) * FR + lrow + 16 * c);
-        }
-        // outline layer: ordinals of outline pixels (atomicMax), 0 elsewhere
-        for (int i = tid; i < RG_BAND * MG_RES / 4; i += RG_THREADS)
-            ((uint4 *)&sm.u.post.band[0][0])[i] = make_uint4(0, 0, 0, 0);
-        if (tid == 0) sm.nlong = 0;
-        if (tid < 64) { // geoms whose rows meet this band, in draw order (ballot compaction)
-            int cnt = 0;
-            for (int base = 0; base < G; base += 64) {
-                const int g = base + lane;
-                bool ov = false;
-                if (g < G) {
-                    const uint4 gi = sm.ginfo[g];
-                    const int ymin = (int16_t)(gi.x & 0xFFFF), ymax = (int16_t)(gi.x >> 16);
-                    const int xmin = (int16_t)(gi.y & 0xFFFF), xmax = (int16_t)(gi.y >> 16);
-                    ov = ymax >= y0 && ymin < y0 + RG_BAND && xmin <= xmax;
-                }
-                const uint64_t m = __ballot(ov);
-                if (ov) {
-                    const int slot = cnt + __popcll(m & ((1ull << lane) - 1ull));
-                    sm.blist[slot] = (int16_t)g;
-                    sm.gslot[g] = (int16_t)slot;
-                }
-                cnt += __popcll(m);
-            }
-            if (lane == 0) sm.nblist = cnt;
-        }
-        RG_SYNC();
         MG_PROF(1);
-#ifdef MG_PROFILE
-        if (tid < 4) sm.pw[tid] = 0u;
-        const int dskip = out.debug_skip;
-#else
-        const int dskip = 0;
-#endif
         MG_PROF_MARK(t_lines);
         // fill spans of this band's rows: each binned fill edge writes its chain's intersection
         // (side 0: edges going down the vertex order, side 1: going up) of the rows it meets here
@@ -622,7 +627,17 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             const int slot = sm.gslot[sm.v_geom[ve & 0x3FFF]];
             int16_t *col = (int16_t *)&sm.bspan[slot][0] + side;
             const int ra = r0 > y0 ? r0 : y0, rb = r1 < y0 + RG_BAND - 1 ? r1 : y0 + RG_BAND - 1;
-            for (int y = ra; y <= rb; y++) col[2 * (y - y0)] = (int16_t)((y - ya) * (xb - xa) / (yb - ya) + xa);
+            if (ra > rb) continue;
+            // x = xa + trunc((y - ya) * (xb - xa) / (yb - ya)), stepped row by row (y >= ya, yb > ya)
+            const int d = yb - ya, adx = xb > xa ? xb - xa : xa - xb, sg = xb >= xa ? 1 : -1;
+            const int n0 = (ra - ya) * adx;
+            int q = n0 / d, r = n0 - q * d;
+            const int qs = adx / d, rs = adx - qs * d;
+            for (int y = ra; y <= rb; y++) {
+                col[2 * (y - y0)] = (int16_t)(xa + sg * q);
+                q += qs; r += rs;
+                if (r >= d) { r -= d; q++; }
+            }
         }
         // outline items of this band: solid width-2 edges (clip_and_draw_line_width: base line plus one
         // offset copy, each clipped) and clipped dashed-goal lines
@@ -722,51 +737,61 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             }
         }
         MG_PROF_MAXW(sm.pw[1], t_fill);
-        if (mode == 1) {
-            RG_SYNC();
-            for (int i = tid; i < nbl * RG_BAND; i += RG_THREADS)
-                (&sm.bspan[0][0])[i] = (uint32_t)RG_EMPTY | ((uint32_t)RG_EMPTY << 16);
-            continue;
-        }
         if (do_pf) sm.u.post.past[tid / RG_BANDLO16][tid % RG_BANDLO16] = pf;
         RG_SYNC();
         MG_PROF(3);
 #ifdef MG_PROFILE
         _pacc[5] += sm.pw[0]; _pacc[6] += sm.pw[1]; _pacc[7] += nlong; _pacc[8] += sm.bin_off[band_i + 1] - sm.bin_off[band_i];
         _pacc[9] += nbl;
+        if (tid < 4) sm.pw[tid] = 0u;
 #endif
-        for (int i = tid; i < nbl * RG_BAND; i += RG_THREADS)  // band spans back to empty for the next band
+        // tail: this band's outputs (wave 0: frame stack, waves 1-2: ring + current frame), and the
+        // next band's empty spans, cleared outline layer, band list (wave 2) and prefetch
+        for (int i = tid; i < nbl * RG_BAND; i += RG_THREADS)
             (&sm.bspan[0][0])[i] = (uint32_t)RG_EMPTY | ((uint32_t)RG_EMPTY << 16);
-        // ring of the last 4 LoRes frames: slot nh (all 4 slots at episode start)
-        for (int t = tid; keep_ring && t < (fresh ? 4 : 1) * RG_BANDLO16 && !(dskip & 4); t += RG_THREADS) {
-            int sl = fresh ? t / RG_BANDLO16 : nh, c = t % RG_BANDLO16;
-            *(uint4 *)(ring + ((size_t)sl * S.N + e) * FR + lrow + 16 * c) = sm.u.post.lo[c];
+        for (int i = tid; i < RG_BAND * MG_RES / 4; i += RG_THREADS)
+            ((uint4 *)&sm.u.post.band[0][0])[i] = make_uint4(0, 0, 0, 0);
+        if (tid == 0) sm.nlong = 0;
+        if (mode == 0 && !(dskip & 4)) {
+            if (tid >= 64) {
+                // ring of the last 4 LoRes frames: slot nh (all 4 slots at episode start)
+                const int nring = keep_ring ? (fresh ? 4 : 1) * RG_BANDLO16 : 0;
+                for (int t = tid - 64; t < nring + (plain ? RG_BANDLO16 : 0); t += RG_THREADS - 64) {
+                    if (t < nring) {
+                        const int sl = fresh ? t / RG_BANDLO16 : nh, c = t % RG_BANDLO16;
+                        *(uint4 *)(ring + ((size_t)sl * S.N + e) * FR + lrow + 16 * c) = sm.u.post.lo[c];
+                    } else {
+                        const int c = t - nring;
+                        *(uint4 *)(o_plain + (size_t)e * FR + lrow + 16 * c) = sm.u.post.lo[c];
+                    }
+                }
+            } else if (stacked && tid < 2 * MG_LORES / 4) {
+                // FlattenFrameStack: [96][96][12] = frames oldest..newest concatenated per pixel; one thread
+                // per 4 pixels: 3 dwords of each frame in, 12 dwords (3 x 16 B) out
+                const uint32_t *p32 = (const uint32_t *)sm.u.post.past, *c32 = (const uint32_t *)sm.u.post.lo;
+                uint32_t f[4][3];
+#pragma unroll
+                for (int w = 0; w < 3; w++) {
+                    f[3][w] = c32[3 * tid + w];
+#pragma unroll
+                    for (int k = 0; k < 3; k++) f[k][w] = fresh ? f[3][w] : p32[k * (RG_BANDLO / 4) + 3 * tid + w];
+                }
+                uint32_t o[12];
+#pragma unroll
+                for (int b = 0; b < 48; b++) {   // output byte b: pixel b / 12, frame (b % 12) / 3, channel b % 3
+                    const int px = b / 12, k = (b % 12) / 3, sb = 3 * px + b % 3;  // source byte within 12
+                    const uint32_t byte = (f[k][sb / 4] >> (8 * (sb % 4))) & 255u;
+                    if (b % 4 == 0) o[b / 4] = byte; else o[b / 4] |= byte << (8 * (b % 4));
+                }
+                uint4 *dst = (uint4 *)(o_stack + (size_t)e * FR * 4 + lrow * 4) + 3 * tid;
+                dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+                dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+                dst[2] = make_uint4(o[8], o[9], o[10], o[11]);
+            }
         }
-        if (plain && !(dskip & 4))
-            for (int c = tid; c < RG_BANDLO16; c += RG_THREADS)
-                *(uint4 *)(o_plain + (size_t)e * FR + lrow + 16 * c) = sm.u.post.lo[c];
-        if (stacked && !(dskip & 4) && tid < 2 * MG_LORES / 4) {
-            // FlattenFrameStack: [96][96][12] = frames oldest..newest concatenated per pixel; one thread
-            // per 4 pixels: 3 dwords of each frame in, 12 dwords (3 x 16 B) out
-            const uint32_t *p32 = (const uint32_t *)sm.u.post.past, *c32 = (const uint32_t *)sm.u.post.lo;
-            uint32_t f[4][3];
-#pragma unroll
-            for (int w = 0; w < 3; w++) {
-                f[3][w] = c32[3 * tid + w];
-#pragma unroll
-                for (int k = 0; k < 3; k++) f[k][w] = fresh ? f[3][w] : p32[k * (RG_BANDLO / 4) + 3 * tid + w];
-            }
-            uint32_t o[12];
-#pragma unroll
-            for (int b = 0; b < 48; b++) {   // output byte b: pixel b / 12, frame (b % 12) / 3, channel b % 3
-                const int px = b / 12, k = (b % 12) / 3, sb = 3 * px + b % 3;  // source byte within 12
-                const uint32_t byte = (f[k][sb / 4] >> (8 * (sb % 4))) & 255u;
-                if (b % 4 == 0) o[b / 4] = byte; else o[b / 4] |= byte << (8 * (b % 4));
-            }
-            uint4 *dst = (uint4 *)(o_stack + (size_t)e * FR * 4 + lrow * 4) + 3 * tid;
-            dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
-            dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
-            dst[2] = make_uint4(o[8], o[9], o[10], o[11]);
+        if (y0 + RG_BAND < MG_RES) {
+            if (tid >= 128) band_list(y0 + RG_BAND);
+            if (do_pf) pf = prefetch(y0 + RG_BAND);
         }
         RG_SYNC();
         MG_PROF(4);
