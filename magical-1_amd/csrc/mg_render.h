@@ -620,7 +620,10 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         // fill spans of this band's rows: each binned fill edge writes its chain's intersection
         // (side 0: edges going down the vertex order, side 1: going up) of the rows it meets here
         const int nbl = sm.nblist;
-        for (int j = sm.ebin_off[band_i] + nout + tid; j < sm.ebin_off[band_i + 1] + nout && !(dskip & 8); j += RG_THREADS) {
+        // (wave 1; the outline items run on waves 0 and 2 at the same time)
+        const bool fwave = tid >= 64 && tid < 128;
+        const int lt = tid < 64 ? tid : tid - 64;   // outline-item thread index (waves 0, 2)
+        for (int j = sm.ebin_off[band_i] + nout + tid - 64; fwave && j < sm.ebin_off[band_i + 1] + nout && !(dskip & 8); j += 64) {
             const int ve = sm.bin[j];
             int xa, ya, xb, yb, side, r0, r1;
             fill_edge(sm, ve, xa, ya, xb, yb, side, r0, r1);
@@ -642,7 +645,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         // outline items of this band: solid width-2 edges (clip_and_draw_line_width: base line plus one
         // offset copy, each clipped) and clipped dashed-goal lines
         // (one thread per segment: solid edges contribute two, dash lines one)
-        for (int j2 = 2 * sm.bin_off[band_i] + tid; j2 < 2 * sm.bin_off[band_i + 1] && !(dskip & 1); j2 += RG_THREADS) {
+        for (int j2 = 2 * sm.bin_off[band_i] + lt; !fwave && j2 < 2 * sm.bin_off[band_i + 1] && !(dskip & 1); j2 += 128) {
             const int i = sm.bin[j2 >> 1], c = j2 & 1;
             int x1, y1, x2, y2;
             uint32_t ord;
