@@ -29,7 +29,8 @@
 #define RG_BAND 8
 #define RG_NBANDS (MG_RES / RG_BAND)
 #define RG_THREADS 192                  // = one thread per 4x4 block of a band (2 x 96)
-#define RG_SHORT 16                     // segments with <= RG_SHORT pixels in a band: drawn by their own thread
+#define RG_SHORT 12                     // segments with <= RG_SHORT * RG_SEGLANES pixels in a band: drawn by
+#define RG_SEGLANES 4                   // their own group of RG_SEGLANES lanes
 #define RG_EMPTY 32767
 #define RG_LOROW (MG_LORES * 3)         // bytes of one 96-px RGB row
 #define RG_BANDLO (2 * RG_LOROW)        // bytes of the 2 LoRes rows one band produces
@@ -261,14 +262,22 @@ MG_DEV void raster_krange(SM &sm, const LineK &L, int ka, int kb, int y0, uint32
     }
 }
 
-// one clipped segment: short runs are drawn here, long runs are queued for the whole workgroup
+// one clipped segment, drawn by a group of RG_SEGLANES lanes (lane sub of the group takes one
+// contiguous part of the band's pixel run); long runs are queued for the whole workgroup
 template <class SM>
-MG_DEV void segment_band(SM &sm, int x1, int y1, int x2, int y2, uint32_t ord, int y0) {
+MG_DEV void segment_band(SM &sm, int x1, int y1, int x2, int y2, uint32_t ord, int y0, int sub) {
     int klo, khi;
     const LineK L = line_k(x1, y1, x2, y2);
     band_krange(L, y0, klo, khi);
     if (khi < klo) return;
-    if (khi - klo + 1 > RG_SHORT) {
+    const int n = khi - klo + 1;
+    if (n <= RG_SHORT * RG_SEGLANES) {
+        const int chunk = (n + RG_SEGLANES - 1) / RG_SEGLANES;
+        const int ka = klo + sub * chunk, kb = ka + chunk - 1 < khi ? ka + chunk - 1 : khi;
+        if (ka <= kb) raster_krange(sm, L, ka, kb, y0, ord);
+        return;
+    }
+    if (sub == 0) {
         int q = atomicAdd(&sm.nlong, 1);
         if (q < RG_MAXLONG) {
             int32_t *d = sm.u.post.lk[q];
@@ -276,8 +285,8 @@ MG_DEV void segment_band(SM &sm, int x1, int y1, int x2, int y2, uint32_t ord, i
             sm.u.post.lkr[q][0] = klo; sm.u.post.lkr[q][1] = khi; sm.u.post.lkr[q][2] = (int32_t)ord;
             return;
         }
+        raster_krange(sm, L, klo, khi, y0, ord);   // queue full: drawn here
     }
-    raster_krange(sm, L, klo, khi, y0, ord);
 }
 
 // end points of solid outline edge k: (float->int first point) -> (int next vertex)
@@ -645,7 +654,8 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         // outline items of this band: solid width-2 edges (clip_and_draw_line_width: base line plus one
         // offset copy, each clipped) and clipped dashed-goal lines
         // (one thread per segment: solid edges contribute two, dash lines one)
-        for (int j2 = 2 * sm.bin_off[band_i] + lt; !fwave && j2 < 2 * sm.bin_off[band_i + 1] && !(dskip & 1); j2 += 128) {
+        for (int j2 = 2 * sm.bin_off[band_i] + lt / RG_SEGLANES; !fwave && j2 < 2 * sm.bin_off[band_i + 1] && !(dskip & 1);
+             j2 += 128 / RG_SEGLANES) {
             const int i = sm.bin[j2 >> 1], c = j2 & 1;
             int x1, y1, x2, y2;
             uint32_t ord;
@@ -664,7 +674,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
                 ord = (uint32_t)sm.dash_o[i - nsedge];
             }
             if (clip && !clipline(x1, y1, x2, y2)) continue;
-            segment_band(sm, x1, y1, x2, y2, ord, y0);
+            segment_band(sm, x1, y1, x2, y2, ord, y0, lt % RG_SEGLANES);
         }
         MG_PROF_MAXW(sm.pw[0], t_lines);
         RG_SYNC();
