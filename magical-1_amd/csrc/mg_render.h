@@ -25,7 +25,7 @@
 // robot + arena + goal + one block (MoveToRegion / MoveToCorner) and leaves room for 5 workgroups/CU.
 #define RG_LARGE 160, 1600, 256, 3072
 #define RG_SMALL 32, 704, 160, 1536
-#define RG_MAXLONG 64
+#define RG_MAXLONG 16
 #define RG_BAND 8
 #define RG_NBANDS (MG_RES / RG_BAND)
 #define RG_THREADS 192                  // = one thread per 4x4 block of a band (2 x 96)
@@ -57,7 +57,6 @@ struct RenderSmem {
         struct {
             uint32_t band[RG_BAND][MG_RES]; // outline layer of the current band
             uint4 lo[RG_BANDLO16];          // current frame, 2 LoRes rows
-            uint4 past[3][RG_BANDLO16];     // frames t-3, t-2, t-1 of the same rows
             int32_t lk[RG_MAXLONG][7];      // long segments of this band (LineK)
             int32_t lkr[RG_MAXLONG][3];     // klo, khi, ordinal
         } post;
@@ -578,16 +577,24 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     uint8_t *o_plain = view == 0 ? out.obs_allo : out.obs_ego;
     uint8_t *o_stack = pp == MG_PREPROC_LORESSTACK ? o_plain : out.obs_past;
     const int oyl = tid / MG_LORES, ox = tid % MG_LORES, x0 = 4 * ox;
-    const bool do_pf = mode == 0 && stacked && !fresh && tid < 3 * RG_BANDLO16;
+    // frame-stack threads (4 pixels each) hold frames t-3..t-1 of their pixels in registers
+    const bool do_pf = mode == 0 && stacked && !fresh && tid < 2 * MG_LORES / 4;
 #ifdef MG_PROFILE
     const int dskip = out.debug_skip;
 #else
     const int dskip = 0;
 #endif
-    // prefetch frames t-3..t-1 of band y0's rows (ring slots nh+1..nh+3, never written this step)
+    // prefetch frames t-3..t-1 of this thread's 4 pixels of band y0 (ring slots nh+1..nh+3, never
+    // written this step): 3 dwords per frame
+    uint32_t pf[3][3];
     auto prefetch = [&](int y0) {
-        int k = tid / RG_BANDLO16, c = tid % RG_BANDLO16, sl = (nh + 1 + k) & 3;
-        return *(const uint4 *)(ring + ((size_t)sl * S.N + e) * FR + (size_t)(y0 / 4) * RG_LOROW + 16 * c);
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const int sl = (nh + 1 + k) & 3;
+            const uint32_t *src = (const uint32_t *)(ring + ((size_t)sl * S.N + e) * FR + (size_t)(y0 / 4) * RG_LOROW) + 3 * tid;
+#pragma unroll
+            for (int w = 0; w < 3; w++) pf[k][w] = src[w];
+        }
     };
     // geoms whose rows meet band y0, in draw order (ballot compaction by one wave)
     auto band_list = [&](int y0) {
@@ -612,8 +619,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         if (lane == 0) sm.nblist = cnt;
     };
     // band 0 prologue: outline layer cleared, band list, prefetch (later bands: in the previous band's tail)
-    uint4 pf = make_uint4(0, 0, 0, 0);
-    if (do_pf) pf = prefetch(0);
+    if (do_pf) prefetch(0);
     for (int i = tid; i < RG_BAND * MG_RES / 4; i += RG_THREADS)
         ((uint4 *)&sm.u.post.band[0][0])[i] = make_uint4(0, 0, 0, 0);
     if (tid == 0) sm.nlong = 0;
@@ -750,7 +756,6 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             }
         }
         MG_PROF_MAXW(sm.pw[1], t_fill);
-        if (do_pf) sm.u.post.past[tid / RG_BANDLO16][tid % RG_BANDLO16] = pf;
         RG_SYNC();
         MG_PROF(3);
 #ifdef MG_PROFILE
@@ -781,13 +786,13 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             } else if (stacked && tid < 2 * MG_LORES / 4) {
                 // FlattenFrameStack: [96][96][12] = frames oldest..newest concatenated per pixel; one thread
                 // per 4 pixels: 3 dwords of each frame in, 12 dwords (3 x 16 B) out
-                const uint32_t *p32 = (const uint32_t *)sm.u.post.past, *c32 = (const uint32_t *)sm.u.post.lo;
+                const uint32_t *c32 = (const uint32_t *)sm.u.post.lo;
                 uint32_t f[4][3];
 #pragma unroll
                 for (int w = 0; w < 3; w++) {
                     f[3][w] = c32[3 * tid + w];
 #pragma unroll
-                    for (int k = 0; k < 3; k++) f[k][w] = fresh ? f[3][w] : p32[k * (RG_BANDLO / 4) + 3 * tid + w];
+                    for (int k = 0; k < 3; k++) f[k][w] = fresh ? f[3][w] : pf[k][w];
                 }
                 uint32_t o[12];
 #pragma unroll
@@ -804,7 +809,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         }
         if (y0 + RG_BAND < MG_RES) {
             if (tid >= 128) band_list(y0 + RG_BAND);
-            if (do_pf) pf = prefetch(y0 + RG_BAND);
+            if (do_pf) prefetch(y0 + RG_BAND);
         }
         RG_SYNC();
         MG_PROF(4);
