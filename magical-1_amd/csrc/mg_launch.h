@@ -24,9 +24,11 @@ struct StepCaps { int nb, ns, nc, na, blk; };
 size_t mg_step_lds_bytes(const StepCaps &c, int blk);
 // compiled LDS variant matching these caps for n_envs (0: the HBM-state kernel)
 int mg_step_variant(const StepCaps &c, int n_envs);
-hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, int variant, int max_steps, int auto_reset,
-                          const uint8_t *actions, float *reward, uint8_t *done, double *eval_score, uint8_t *reset_mask,
-                          hipStream_t st);
+// compiled envs-per-workgroup sizes of a variant
+bool mg_step_blk_ok(int variant, int blk);
+hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, int variant, int blk, int max_steps,
+                          int auto_reset, const uint8_t *actions, float *reward, uint8_t *done, double *eval_score,
+                          uint8_t *reset_mask, hipStream_t st);
 hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderOut &ro, int mode, hipStream_t st);
 hipError_t mg_launch_compose3ea(const MGState &S, const uint8_t *obs_allo, const uint8_t *mask, uint8_t *obs_past,
                                 hipStream_t st);

@@ -141,18 +141,39 @@ __host__ __device__ constexpr StepCaps step_variant_caps(int v) {
          : StepCaps{0, 0, 0, 0, 0};
 }
 
-template <int VAR>
+// Workgroups are dispatched round-robin over the 8 XCDs (workgroup b -> XCD b % 8); map them so
+// that each XCD owns one contiguous range of envs: neighbouring envs share [slot][N] cache lines,
+// and with few envs per workgroup those lines are then reused in the XCD's own L2.
+__device__ __forceinline__ int xcd_block(int b, int g) {
+    const int q = g >> 3, r = g & 7, x = b & 7;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+
+// Robot.set_action + 10 x (Robot.update, cpSpaceStep): base_env.py:248-276
+template <int NCS>
+__device__ __forceinline__ void env_substeps(const MGState &V, const mg_library *L, int ev, int a, MGProf &P) {
+    robot_set_action(V, L, ev, a < 18 ? a : 0);
+    const double dt = L->dt;
+    for (int i = 0; i < 10; i++) {
+        robot_update(V, L, ev);
+        MG_PP(P, 0);
+        space_step<NCS>(V, L, ev, dt, P);
+    }
+}
+
+template <int VAR, int BLK>
 __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg, int max_steps,
                                                   int auto_reset, const uint8_t *__restrict__ actions, float *reward,
                                                   uint8_t *done, double *eval_score, uint8_t *reset_mask) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr StepCaps C = step_variant_caps(VAR);
     constexpr bool LDS = VAR != 0;
-    const int lane = threadIdx.x, e = blockIdx.x * blockDim.x + lane;
+    const int lane = BLK == 1 ? 0 : threadIdx.x, e = xcd_block(blockIdx.x, gridDim.x) * BLK + lane;
     if (e >= S.n_envs) return;
-    MGState V = S;
-    int ev = e;
-    if (LDS) {
+    const int a = actions[e];
+    MGProf P;
+    MG_PP_INIT(P);
+    if constexpr (LDS) {
         if (S.nbodies[e] > C.nb || S.nshapes[e] > C.ns || S.ncons[e] > C.nc) {
             S.overflow[e] |= 16; // scene larger than the variant's LDS caps (never expected)
             if (reset_mask) reset_mask[e] = 0;
@@ -168,21 +189,16 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
             if (reset_mask) reset_mask[e] = 0;
             return;
         }
-        carve_view(V, smem, C, C.blk);
+        // the view is built from the LDS carve only (never merged with the HBM pointers), so every
+        // access through it compiles to ds_* with a constant offset from the lane's column
+        MGState V = S;
+        carve_view(V, smem, C, BLK);
         xfer_state(S, V, C, lane, e, true);
-        ev = lane;
+        env_substeps<C.nc>(V, L, lane, a, P);
+        xfer_state(S, V, C, lane, e, false);
+    } else {
+        env_substeps<0>(S, L, e, a, P);
     }
-    const int a = actions[e];
-    robot_set_action(V, L, ev, a < 18 ? a : 0);
-    const double dt = L->dt;
-    MGProf P;
-    MG_PP_INIT(P);
-    for (int i = 0; i < 10; i++) {
-        robot_update(V, L, ev);
-        MG_PP(P, 0);
-        space_step<LDS ? C.nc : 0>(V, L, ev, dt, P);
-    }
-    if (LDS) xfer_state(S, V, C, lane, e, false);
     int steps = S.episode_steps[e] + 1;
     S.episode_steps[e] = steps;
     bool d = max_steps > 0 && steps >= max_steps;
@@ -228,44 +244,48 @@ hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, c
 }
 
 int mg_step_variant(const StepCaps &c, int n_envs) {
+    (void)n_envs;
     for (int v = 1; v <= 2; v++) {
         const StepCaps k = step_variant_caps(v);
-        if (c.nb == k.nb && c.ns == k.ns && c.nc == k.nc && c.na == k.na && n_envs <= k.blk * 256) return v;
+        if (c.nb == k.nb && c.ns == k.ns && c.nc == k.nc && c.na == k.na) return v;
     }
     return 0;
 }
 
-template <int VAR>
+template <int VAR, int BLK>
 static hipError_t launch_step_var(const MGState &S, const mg_library *L, TaskCfg cfg, int max_steps, int auto_reset,
                                   const uint8_t *actions, float *reward, uint8_t *done, double *eval_score,
                                   uint8_t *reset_mask, hipStream_t st) {
     constexpr StepCaps C = step_variant_caps(VAR);
-    if (VAR == 0) {
-        hipLaunchKernelGGL(step_kernel<VAR>, dim3((S.n_envs + 63) / 64), dim3(64), 0, st, S, L, cfg, max_steps, auto_reset,
-                           actions, reward, done, eval_score, reset_mask);
-        return hipGetLastError();
-    }
+    const size_t lds = VAR == 0 ? 0 : mg_step_lds_bytes(C, BLK);
     static bool attr_set = false;
-    const size_t lds = mg_step_lds_bytes(C, C.blk);
-    if (!attr_set) {
-        hipError_t err = hipFuncSetAttribute((const void *)step_kernel<VAR>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)lds);
+    if (VAR != 0 && !attr_set) {
+        hipError_t err = hipFuncSetAttribute((const void *)step_kernel<VAR, BLK>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (err != hipSuccess) return err;
         attr_set = true;
     }
-    hipLaunchKernelGGL(step_kernel<VAR>, dim3((S.n_envs + C.blk - 1) / C.blk), dim3(C.blk), lds, st, S, L, cfg, max_steps,
-                       auto_reset, actions, reward, done, eval_score, reset_mask);
+    hipLaunchKernelGGL((step_kernel<VAR, BLK>), dim3((S.n_envs + BLK - 1) / BLK), dim3(BLK), lds, st, S, L, cfg,
+                       max_steps, auto_reset, actions, reward, done, eval_score, reset_mask);
     return hipGetLastError();
 }
 
-hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, int variant, int max_steps, int auto_reset,
-                          const uint8_t *actions, float *reward, uint8_t *done, double *eval_score, uint8_t *reset_mask,
-                          hipStream_t st) {
-    switch (variant) {
-    case 1: return launch_step_var<1>(S, L, cfg, max_steps, auto_reset, actions, reward, done, eval_score, reset_mask, st);
-    case 2: return launch_step_var<2>(S, L, cfg, max_steps, auto_reset, actions, reward, done, eval_score, reset_mask, st);
-    default: return launch_step_var<0>(S, L, cfg, max_steps, auto_reset, actions, reward, done, eval_score, reset_mask, st);
-    }
+// envs per workgroup: compiled sizes only
+bool mg_step_blk_ok(int variant, int blk) {
+    return variant == 0 ? (blk == 1 || blk == 8 || blk == 64) : (blk == 1 || blk == 4 || blk == 16);
+}
+
+hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, int variant, int blk, int max_steps,
+                          int auto_reset, const uint8_t *actions, float *reward, uint8_t *done, double *eval_score,
+                          uint8_t *reset_mask, hipStream_t st) {
+#define MG_STEP_CASE(V, B) \
+    if (variant == V && blk == B) \
+        return launch_step_var<V, B>(S, L, cfg, max_steps, auto_reset, actions, reward, done, eval_score, reset_mask, st);
+    MG_STEP_CASE(1, 1) MG_STEP_CASE(1, 4) MG_STEP_CASE(1, 16)
+    MG_STEP_CASE(2, 1) MG_STEP_CASE(2, 4) MG_STEP_CASE(2, 16)
+    MG_STEP_CASE(0, 1) MG_STEP_CASE(0, 8) MG_STEP_CASE(0, 64)
+#undef MG_STEP_CASE
+    return hipErrorInvalidValue;
 }
 
 hipError_t mg_prof_read_physics(unsigned long long *out) {

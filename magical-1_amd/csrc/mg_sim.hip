@@ -37,6 +37,7 @@ struct mg_sim {
     int bound;
     StepCaps caps;     // the task's per-env slot caps
     int step_variant;  // compiled LDS-resident step variant (0: HBM state)
+    int step_blk;      // envs per step workgroup
     uint8_t *reset_mask; // device u8[N]: envs to auto-reset after the step
     // optional per-kernel timing (hipEvents on the launch stream)
     int timing;
@@ -181,6 +182,13 @@ static int pick_step_variant(const StepCaps &c, int n_envs) {
     return v;
 }
 
+static int pick_step_blk(int variant) {
+    int b = variant == 0 ? 64 : 16;
+    const char *ov = getenv(variant == 0 ? "MG_STEP_BLK0" : "MG_STEP_BLK"); // experiments
+    if (ov && mg_step_blk_ok(variant, atoi(ov))) b = atoi(ov);
+    return b;
+}
+
 static int grid64(const mg_sim *s) { return (s->S.n_envs + 63) / 64; }
 
 static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
@@ -249,6 +257,7 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     HIPC(hipMemcpy(s->dlib, cfg->library, sizeof(mg_library), hipMemcpyHostToDevice));
     s->caps = step_caps(cfg->task, cfg->rand_flags, cfg->num_envs, *(const mg_library *)cfg->library);
     s->step_variant = pick_step_variant(s->caps, cfg->num_envs);
+    s->step_blk = pick_step_blk(s->step_variant);
     err = hipMalloc((void **)&s->reset_mask, (size_t)s->S.N);
     if (err != hipSuccess) { (void)hipFree(s->pool); (void)hipFree(s->dlib); delete s; return set_err(-12, "mg_create: hipMalloc mask"); }
     HIPC(hipMemset(s->reset_mask, 0, (size_t)s->S.N));
@@ -305,7 +314,7 @@ int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
     hipEvent_t *ev = nullptr;
     if (s->timing && s->ev_used + 3 <= s->ev.size()) { ev = &s->ev[s->ev_used]; s->ev_used += 3; }
     if (ev) HIPC(hipEventRecord(ev[0], st));
-    HIPC(mg_launch_step(s->S, s->dlib, cfg, s->step_variant, s->max_steps, s->auto_reset, actions, s->out.reward,
+    HIPC(mg_launch_step(s->S, s->dlib, cfg, s->step_variant, s->step_blk, s->max_steps, s->auto_reset, actions, s->out.reward,
                         s->out.done, s->out.eval_score, s->reset_mask, st));
     if (s->auto_reset) HIPC(mg_launch_reset(s->S, s->dlib, cfg, s->reset_mask, st));
     if (ev) HIPC(hipEventRecord(ev[1], st));

@@ -352,6 +352,295 @@ MG_DEV void arbiter_apply(const MGState &S, int e, int slot) {
     }
 }
 
+// ---- register-resident solver sweep (LDS variants) -----------------------
+// With the constraint list known at compile time, applyCachedImpulse and the 10 solver
+// iterations run on body velocities and constraint terms held in VGPRs: constraints index
+// bodies by constants, arbiters (runtime body slots) through select chains.  Same operations
+// in the same order as cons_cached_impl / cons_apply_impl / arbiter_cached / arbiter_apply.
+template <int NB>
+struct RegBodies { double vx[NB], vy[NB], w[NB], vbx[NB], vby[NB], wb[NB], minv[NB], iinv[NB]; };
+
+struct RegCons {
+    double r1x, r1y, r2x, r2y, k11, k12, k21, k22, bias, bias2, jacc, jacc2, jmax, ratio, ratio_inv, isum, rate, twrn,
+        wcoef;
+};
+
+template <int NB>
+MG_DEV double rsel(const double (&x)[NB], int b) {
+    double r = 0.0;
+#pragma unroll
+    for (int k = 0; k < NB; k++) r = b == k ? x[k] : r;
+    return r;
+}
+template <int NB>
+MG_DEV void rput(double (&x)[NB], int b, double v) {
+#pragma unroll
+    for (int k = 0; k < NB; k++) x[k] = b == k ? v : x[k];
+}
+
+// runtime body slot (arbiters)
+template <int NB>
+MG_DEV void rapply_dyn(RegBodies<NB> &R, int b, double minv, double iinv, V2 j, V2 r) {
+    if (b < 0) return;
+    rput(R.vx, b, rsel(R.vx, b) + j.x * minv);
+    rput(R.vy, b, rsel(R.vy, b) + j.y * minv);
+    rput(R.w, b, rsel(R.w, b) + iinv * vcross(r, j));
+}
+template <int NB>
+MG_DEV void rapply_bias_dyn(RegBodies<NB> &R, int b, double minv, double iinv, V2 j, V2 r) {
+    if (b < 0) return;
+    rput(R.vbx, b, rsel(R.vbx, b) + j.x * minv);
+    rput(R.vby, b, rsel(R.vby, b) + j.y * minv);
+    rput(R.wb, b, rsel(R.wb, b) + iinv * vcross(r, j));
+}
+// compile-time body slot (constraints; b < 0 = the static body)
+template <int NB>
+MG_DEV void rapply(RegBodies<NB> &R, int b, V2 j, V2 r) {
+    if (b < 0) return;
+    R.vx[b] = R.vx[b] + j.x * R.minv[b];
+    R.vy[b] = R.vy[b] + j.y * R.minv[b];
+    R.w[b] += R.iinv[b] * vcross(r, j);
+}
+template <int NB> MG_DEV V2 rv(const RegBodies<NB> &R, int b) { return b < 0 ? v2(0.0, 0.0) : v2(R.vx[b], R.vy[b]); }
+template <int NB> MG_DEV double rw(const RegBodies<NB> &R, int b) { return b < 0 ? 0.0 : R.w[b]; }
+template <int NB> MG_DEV double rii(const RegBodies<NB> &R, int b) { return b < 0 ? 0.0 : R.iinv[b]; }
+
+template <int NB>
+MG_DEV void rb_load(RegBodies<NB> &R, const MGState &S, int e) {
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        R.vx[b] = AT(S.bvx, b); R.vy[b] = AT(S.bvy, b); R.w[b] = AT(S.bw, b);
+        R.vbx[b] = AT(S.bvbx, b); R.vby[b] = AT(S.bvby, b); R.wb[b] = AT(S.bwb, b);
+        R.minv[b] = AT(S.bminv, b); R.iinv[b] = AT(S.biinv, b);
+    }
+}
+template <int NB>
+MG_DEV void rb_store(const RegBodies<NB> &R, const MGState &S, int e) {
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        AT(S.bvx, b) = R.vx[b]; AT(S.bvy, b) = R.vy[b]; AT(S.bw, b) = R.w[b];
+        AT(S.bvbx, b) = R.vbx[b]; AT(S.bvby, b) = R.vby[b]; AT(S.bwb, b) = R.wb[b];
+    }
+}
+
+MG_DEV void rc_load(RegCons &q, const MGState &S, int e, int c, int type, double dt) {
+    q.jacc = CPA(CP_JACC, c); q.jacc2 = 0.0; q.jmax = CPA(CP_MAXF, c) * dt;
+    q.isum = CPA(CP_ISUM, c); q.bias = CPA(CP_BIAS, c);
+    if (type == MG_C_PIVOT) {
+        q.jacc2 = CPA(CP_JACC2, c); q.bias2 = CPA(CP_BIAS2, c);
+        q.r1x = CPA(CP_R1X, c); q.r1y = CPA(CP_R1Y, c); q.r2x = CPA(CP_R2X, c); q.r2y = CPA(CP_R2Y, c);
+        q.k11 = CPA(CP_K11, c); q.k12 = CPA(CP_K12, c); q.k21 = CPA(CP_K21, c); q.k22 = CPA(CP_K22, c);
+    }
+    if (type == MG_C_GEAR) { q.ratio = CPA(CP_RATIO, c); q.ratio_inv = CPA(CP_RATIO_INV, c); }
+    if (type == MG_C_MOTOR) q.rate = CPA(CP_RATE, c);
+    if (type == MG_C_SPRING) { q.twrn = CPA(CP_TWRN, c); q.wcoef = CPA(CP_WCOEF, c); }
+}
+MG_DEV void rc_store(const RegCons &q, const MGState &S, int e, int c, int type) {
+    CPA(CP_JACC, c) = q.jacc;
+    if (type == MG_C_PIVOT) CPA(CP_JACC2, c) = q.jacc2;
+    if (type == MG_C_SPRING) CPA(CP_TWRN, c) = q.twrn;
+}
+
+template <int NB>
+MG_DEV void rcons_cached(RegBodies<NB> &R, const RegCons &q, int a, int b, int type, double dt_coef) {
+    switch (type) {
+    case MG_C_PIVOT: {
+        V2 j = vmult(v2(q.jacc, q.jacc2), dt_coef);
+        rapply(R, a, vneg(j), v2(q.r1x, q.r1y));
+        rapply(R, b, j, v2(q.r2x, q.r2y));
+        break;
+    }
+    case MG_C_GEAR: {
+        double j = q.jacc * dt_coef;
+        if (a >= 0) R.w[a] -= j * R.iinv[a] * q.ratio_inv;
+        if (b >= 0) R.w[b] += j * R.iinv[b];
+        break;
+    }
+    case MG_C_ROTLIMIT:
+    case MG_C_MOTOR: {
+        double j = q.jacc * dt_coef;
+        if (a >= 0) R.w[a] -= j * R.iinv[a];
+        if (b >= 0) R.w[b] += j * R.iinv[b];
+        break;
+    }
+    default: break;
+    }
+}
+
+template <int NB>
+MG_DEV void rcons_apply(RegBodies<NB> &R, RegCons &q, int a, int b, int type) {
+    switch (type) {
+    case MG_C_PIVOT: {
+        V2 r1 = v2(q.r1x, q.r1y), r2 = v2(q.r2x, q.r2y);
+        V2 v1 = vadd(rv(R, a), vmult(vperp(r1), rw(R, a)));
+        V2 v2_ = vadd(rv(R, b), vmult(vperp(r2), rw(R, b)));
+        V2 vr = vsub(v2_, v1);
+        V2 d = vsub(v2(q.bias, q.bias2), vr);
+        V2 j = v2(d.x * q.k11 + d.y * q.k12, d.x * q.k21 + d.y * q.k22);
+        V2 jOld = v2(q.jacc, q.jacc2);
+        V2 jAcc = vclamp(vadd(jOld, j), q.jmax);
+        q.jacc = jAcc.x; q.jacc2 = jAcc.y;
+        V2 dj = vsub(jAcc, jOld);
+        rapply(R, a, vneg(dj), r1);
+        rapply(R, b, dj, r2);
+        break;
+    }
+    case MG_C_GEAR: {
+        double wr = rw(R, b) * q.ratio - rw(R, a);
+        double j = (q.bias - wr) * q.isum;
+        double jOld = q.jacc;
+        double jAcc = cpclamp(jOld + j, -q.jmax, q.jmax);
+        q.jacc = jAcc;
+        j = jAcc - jOld;
+        if (a >= 0) R.w[a] -= j * R.iinv[a] * q.ratio_inv;
+        if (b >= 0) R.w[b] += j * R.iinv[b];
+        break;
+    }
+    case MG_C_ROTLIMIT: {
+        double bias = q.bias;
+        if (!bias) return;
+        double wr = rw(R, b) - rw(R, a);
+        double j = -(bias + wr) * q.isum;
+        double jOld = q.jacc;
+        double jAcc = bias < 0.0 ? cpclamp(jOld + j, 0.0, q.jmax) : cpclamp(jOld + j, -q.jmax, 0.0);
+        q.jacc = jAcc;
+        j = jAcc - jOld;
+        if (a >= 0) R.w[a] -= j * R.iinv[a];
+        if (b >= 0) R.w[b] += j * R.iinv[b];
+        break;
+    }
+    case MG_C_MOTOR: {
+        double wr = rw(R, b) - rw(R, a) + q.rate;
+        double j = -wr * q.isum;
+        double jOld = q.jacc;
+        double jAcc = cpclamp(jOld + j, -q.jmax, q.jmax);
+        q.jacc = jAcc;
+        j = jAcc - jOld;
+        if (a >= 0) R.w[a] -= j * R.iinv[a];
+        if (b >= 0) R.w[b] += j * R.iinv[b];
+        break;
+    }
+    case MG_C_SPRING: {
+        double wrn = rw(R, a) - rw(R, b);
+        double w_damp = (q.twrn - wrn) * q.wcoef;
+        q.twrn = wrn + w_damp;
+        double j_damp = w_damp * q.isum;
+        q.jacc += j_damp;
+        if (a >= 0) R.w[a] += j_damp * R.iinv[a];
+        if (b >= 0) R.w[b] -= j_damp * R.iinv[b];
+        break;
+    }
+    }
+}
+
+template <int NB>
+MG_DEV void rarb_cached(RegBodies<NB> &R, const MGState &S, int e, int slot, double dt_coef) {
+    if (AT(S.astate, slot) == ARB_FIRST) return;
+    const int a = AT(S.asa, slot), b = AT(S.asb, slot);
+    const double am = rsel(R.minv, a), ai = rsel(R.iinv, a), bm = rsel(R.minv, b), bi = rsel(R.iinv, b);
+    V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
+    int cnt = AT(S.acount, slot);
+    for (int k = 0; k < cnt; k++) {
+        V2 j = vmult(vrotate(n, v2(ACON(k, AC_JN, slot), ACON(k, AC_JT, slot))), dt_coef);
+        rapply_dyn(R, a, am, ai, vneg(j), v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)));
+        rapply_dyn(R, b, bm, bi, j, v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot)));
+    }
+}
+
+template <int NB>
+MG_DEV void rarb_apply(RegBodies<NB> &R, const MGState &S, int e, int slot) {
+    const int a = AT(S.asa, slot), b = AT(S.asb, slot);
+    const double am = rsel(R.minv, a), ai = rsel(R.iinv, a), bm = rsel(R.minv, b), bi = rsel(R.iinv, b);
+    V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
+    double friction = AT(S.au, slot);
+    int cnt = AT(S.acount, slot);
+    for (int k = 0; k < cnt; k++) {
+        double nMass = ACON(k, AC_NMASS, slot);
+        V2 r1 = v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)), r2 = v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot));
+        V2 vb1 = vadd(v2(rsel(R.vbx, a), rsel(R.vby, a)), vmult(vperp(r1), rsel(R.wb, a)));
+        V2 vb2 = vadd(v2(rsel(R.vbx, b), rsel(R.vby, b)), vmult(vperp(r2), rsel(R.wb, b)));
+        V2 v1 = vadd(v2(rsel(R.vx, a), rsel(R.vy, a)), vmult(vperp(r1), rsel(R.w, a)));
+        V2 v2_ = vadd(v2(rsel(R.vx, b), rsel(R.vy, b)), vmult(vperp(r2), rsel(R.w, b)));
+        V2 vr = vsub(v2_, v1);
+        double vbn = vdot(vsub(vb2, vb1), n);
+        double vrn = vdot(vr, n);
+        double vrt = vdot(vr, vperp(n));
+        double jbn = (ACON(k, AC_BIAS, slot) - vbn) * nMass;
+        double jbnOld = ACON(k, AC_JB, slot);
+        double jBias = cpmax(jbnOld + jbn, 0.0);
+        ACON(k, AC_JB, slot) = jBias;
+        double jn = -(0.0 + vrn) * nMass;
+        double jnOld = ACON(k, AC_JN, slot);
+        double jnAcc = cpmax(jnOld + jn, 0.0);
+        ACON(k, AC_JN, slot) = jnAcc;
+        double jtMax = friction * jnAcc;
+        double jt = -vrt * ACON(k, AC_TMASS, slot);
+        double jtOld = ACON(k, AC_JT, slot);
+        double jtAcc = cpclamp(jtOld + jt, -jtMax, jtMax);
+        ACON(k, AC_JT, slot) = jtAcc;
+        V2 jb = vmult(n, jBias - jbnOld);
+        rapply_bias_dyn(R, a, am, ai, vneg(jb), r1);
+        rapply_bias_dyn(R, b, bm, bi, jb, r2);
+        V2 j = vrotate(n, v2(jnAcc - jnOld, jtAcc - jtOld));
+        rapply_dyn(R, a, am, ai, vneg(j), r1);
+        rapply_dyn(R, b, bm, bi, j, r2);
+    }
+}
+
+template <int NCS, int C = 0>
+MG_DEV void rstatic_load(RegCons *q, const MGState &S, int e, double dt) {
+    if constexpr (C < NCS) {
+        rc_load(q[C], S, e, C, static_cons(C).type, dt);
+        rstatic_load<NCS, C + 1>(q, S, e, dt);
+    }
+}
+template <int NCS, int C = 0>
+MG_DEV void rstatic_store(const RegCons *q, const MGState &S, int e) {
+    if constexpr (C < NCS) {
+        rc_store(q[C], S, e, C, static_cons(C).type);
+        rstatic_store<NCS, C + 1>(q, S, e);
+    }
+}
+template <int NCS, int NB, int C = 0>
+MG_DEV void rstatic_cached(RegBodies<NB> &R, const RegCons *q, double dt_coef) {
+    if constexpr (C < NCS) {
+        constexpr ConsDesc d = static_cons(C);
+        rcons_cached(R, q[C], d.a, d.b, d.type, dt_coef);
+        rstatic_cached<NCS, NB, C + 1>(R, q, dt_coef);
+    }
+}
+template <int NCS, int NB, int C = 0>
+MG_DEV void rstatic_apply(RegBodies<NB> &R, RegCons *q) {
+    if constexpr (C < NCS) {
+        constexpr ConsDesc d = static_cons(C);
+        rcons_apply(R, q[C], d.a, d.b, d.type);
+        rstatic_apply<NCS, NB, C + 1>(R, q);
+    }
+}
+
+// bodies of the compile-time scenes: the robot's six, plus the block's
+__host__ __device__ constexpr int static_nbodies(int ncs) { return ncs > 10 ? 7 : 6; }
+
+// applyCachedImpulse + 10 iterations of the LDS variants, register-resident
+template <int NCS>
+MG_DEV void static_solve(const MGState &S, int e, double dt, double dt_coef, int nact, MGProf &P) {
+    constexpr int NB = static_nbodies(NCS);
+    RegBodies<NB> R;
+    RegCons q[NCS];
+    rb_load(R, S, e);
+    rstatic_load<NCS>(q, S, e, dt);
+    for (int i = 0; i < nact; i++) rarb_cached(R, S, e, AT(S.active, i), dt_coef);
+    rstatic_cached<NCS>(R, q, dt_coef);
+    MG_PP(P, 5);
+#pragma unroll 1
+    for (int it = 0; it < 10; it++) {
+        for (int i = 0; i < nact; i++) rarb_apply(R, S, e, AT(S.active, i));
+        rstatic_apply<NCS>(R, q);
+    }
+    rb_store(R, S, e);
+    rstatic_store<NCS>(q, S, e);
+}
+
 // ---- cpSpaceStep -----------------------------------------------------------
 // NCS > 0: the constraint list is the compile-time static_cons(0 .. NCS-1) (asserted by the caller)
 template <int NCS = 0>
@@ -423,6 +712,11 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
     MG_PP(P, 4);
     // velocity integration is the identity here (no gravity, damping 1, no forces)
     double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
+    if constexpr (NCS > 0) {
+        static_solve<NCS>(S, e, dt, dt_coef, nact, P);
+        MG_PP(P, 6);
+        return;
+    }
     for (int i = 0; i < nact; i++) arbiter_cached(S, e, AT(S.active, i), dt_coef);
     if constexpr (NCS > 0) static_cached<NCS>(S, e, dt_coef);
     else for (int c = 0; c < nc; c++) cons_cached(S, e, c, dt_coef);
