@@ -84,7 +84,7 @@ __device__ __forceinline__ void xfer(T *lds, T *hbm, int rows, int blk, int lane
 // warm-start impulses, the live arbiters (key, contacts, warm-start hashes) and the active list.
 // Cached shape BBs and the constraints' pre-step products are recomputed before use.
 __device__ __forceinline__ void xfer_state(const MGState &S, const MGState &V, const StepCaps &c, int lane, int e,
-                                           bool in) {
+                                           bool in, bool cons_list = false) {
     const int blk = V.N, N = S.N;
 #define XF(f, rows) xfer(V.f, S.f, rows, blk, lane, N, e, in)
 #define XS(f, r) do { if (in) V.f[(uint32_t)(r) * blk + lane] = S.f[(uint32_t)(r) * N + e]; \
@@ -128,6 +128,7 @@ __device__ __forceinline__ void xfer_state(const MGState &S, const MGState &V, c
         XF(bminv, c.nb); XF(biinv, c.nb);
         XF(sr, c.ns); XF(su, c.ns); XF(sgroup, c.ns); XF(shash, c.ns); XF(sbody, c.ns); XF(spoly, c.ns);
         XF(nbodies, 1); XF(nshapes, 1); XF(ncons, 1); XF(robot_body0, 1); XF(robot_cons0, 1);
+        if (cons_list) { XF(ctype, c.nc); XF(ca, c.nc); XF(cb, c.nc); } // runtime constraint list
     }
 #undef XS
 #undef XF
@@ -138,6 +139,7 @@ __device__ __forceinline__ void xfer_state(const MGState &S, const MGState &V, c
 __host__ __device__ constexpr StepCaps step_variant_caps(int v) {
     return v == 1 ? StepCaps{6, 5, 10, 20, 16}    // robot only (MoveToRegion)
          : v == 2 ? StepCaps{7, 6, 12, 32, 16}    // robot + one single-shape block (MoveToCorner)
+         : v == 3 ? StepCaps{14, 53, 26, 48, 1}   // up to 8 blocks incl. stars (Cluster*, MatchRegions): runtime lists
          : StepCaps{0, 0, 0, 0, 0};
 }
 
@@ -168,6 +170,7 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr StepCaps C = step_variant_caps(VAR);
     constexpr bool LDS = VAR != 0;
+    constexpr int NCS = VAR == 3 ? 0 : C.nc; // compile-time constraint list (0: the env's runtime list)
     const int lane = BLK == 1 ? 0 : threadIdx.x, e = xcd_block(blockIdx.x, gridDim.x) * BLK + lane;
     if (e >= S.n_envs) return;
     const int a = actions[e];
@@ -179,8 +182,8 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
             if (reset_mask) reset_mask[e] = 0;
             return;
         }
-        bool ok = S.ncons[e] == C.nc && S.robot_body0[e] == 0 && S.robot_cons0[e] == 0;
-        for (int c = 0; c < C.nc; c++) {
+        bool ok = NCS == 0 || (S.ncons[e] == C.nc && S.robot_body0[e] == 0 && S.robot_cons0[e] == 0);
+        for (int c = 0; c < NCS; c++) {
             const ConsDesc d = static_cons(c);
             ok = ok && AT(S.ctype, c) == d.type && AT(S.ca, c) == d.a && AT(S.cb, c) == d.b;
         }
@@ -193,8 +196,8 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
         // access through it compiles to ds_* with a constant offset from the lane's column
         MGState V = S;
         carve_view(V, smem, C, BLK);
-        xfer_state(S, V, C, lane, e, true);
-        env_substeps<C.nc>(V, L, lane, a, P);
+        xfer_state(S, V, C, lane, e, true, NCS == 0);
+        env_substeps<NCS>(V, L, lane, a, P);
         xfer_state(S, V, C, lane, e, false);
     } else {
         env_substeps<0>(S, L, e, a, P);
@@ -249,6 +252,10 @@ int mg_step_variant(const StepCaps &c, int n_envs) {
         const StepCaps k = step_variant_caps(v);
         if (c.nb == k.nb && c.ns == k.ns && c.nc == k.nc && c.na == k.na) return v;
     }
+    // runtime constraint lists: any scene within the caps (arbiter slots must match exactly: the HBM
+    // slots beyond the task's cap are never initialised)
+    const StepCaps k = step_variant_caps(3);
+    if (c.nb <= k.nb && c.ns <= k.ns && c.nc <= k.nc && c.na == k.na) return 3;
     return 0;
 }
 
@@ -272,7 +279,9 @@ static hipError_t launch_step_var(const MGState &S, const mg_library *L, TaskCfg
 
 // envs per workgroup: compiled sizes only
 bool mg_step_blk_ok(int variant, int blk) {
-    return variant == 0 ? (blk == 1 || blk == 8 || blk == 64) : (blk == 1 || blk == 4 || blk == 16);
+    return variant == 0 ? (blk == 1 || blk == 8 || blk == 64)
+         : variant == 3 ? (blk == 1 || blk == 4)
+         : (blk == 1 || blk == 4 || blk == 16);
 }
 
 hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, int variant, int blk, int max_steps,
@@ -283,6 +292,7 @@ hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, in
         return launch_step_var<V, B>(S, L, cfg, max_steps, auto_reset, actions, reward, done, eval_score, reset_mask, st);
     MG_STEP_CASE(1, 1) MG_STEP_CASE(1, 4) MG_STEP_CASE(1, 16)
     MG_STEP_CASE(2, 1) MG_STEP_CASE(2, 4) MG_STEP_CASE(2, 16)
+    MG_STEP_CASE(3, 1) MG_STEP_CASE(3, 4)
     MG_STEP_CASE(0, 1) MG_STEP_CASE(0, 8) MG_STEP_CASE(0, 64)
 #undef MG_STEP_CASE
     return hipErrorInvalidValue;

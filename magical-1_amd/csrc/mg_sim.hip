@@ -172,18 +172,22 @@ static StepCaps step_caps(int task, int flags, int n_envs, const mg_library &lib
     return c;
 }
 
-// LDS views pay off while every env gets its workgroup in a single round of workgroups (one per CU);
-// otherwise the HBM-state kernel (64 envs/wavefront) wins (measured: ClusterColour-Demo x8192 9.4 ms
-// HBM vs 20 ms LDS; MoveToRegion x4096 1.7 ms LDS vs 3.0 ms HBM).
-static int pick_step_variant(const StepCaps &c, int n_envs) {
+// Step kernel per scene (measured on MI355X, 8192 envs, ms per env-step of physics):
+// * compiled constraint lists (robot only / robot + one block): LDS variants 1/2, 16 envs per workgroup;
+// * MatchRegions (1-8 blocks, random per env): LDS variant 3, one env per workgroup, 10.6 ms vs
+//   21.1 ms for the HBM-state kernel, whose 64-env wavefronts diverge on the per-env scene;
+// * Cluster* (8-10 blocks in every env, dense contacts): the HBM-state kernel, 10.7 ms vs 15.1 ms
+//   for variant 3, which fits 8 envs per CU in LDS (19 KB each) and needs 4 rounds of workgroups.
+static int pick_step_variant(const StepCaps &c, int n_envs, int task) {
     int v = mg_step_variant(c, n_envs);
+    if (v == 3 && (task == MG_TASK_CLUSTER_COLOUR || task == MG_TASK_CLUSTER_SHAPE)) v = 0;
     const char *ov = getenv("MG_STEP_VARIANT"); // experiments: force 0 (HBM) or a compiled variant
-    if (ov) { int w = atoi(ov); if (w == 0 || w == v) v = w; }
+    if (ov) { int w = atoi(ov); if (w == 0 || w == mg_step_variant(c, n_envs)) v = w; }
     return v;
 }
 
 static int pick_step_blk(int variant) {
-    int b = variant == 0 ? 64 : 16;
+    int b = variant == 0 ? 64 : variant == 3 ? 1 : 16;
     const char *ov = getenv(variant == 0 ? "MG_STEP_BLK0" : "MG_STEP_BLK"); // experiments
     if (ov && mg_step_blk_ok(variant, atoi(ov))) b = atoi(ov);
     return b;
@@ -256,7 +260,7 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     if (err != hipSuccess) { (void)hipFree(s->pool); delete s; return set_err(-12, "mg_create: hipMalloc library"); }
     HIPC(hipMemcpy(s->dlib, cfg->library, sizeof(mg_library), hipMemcpyHostToDevice));
     s->caps = step_caps(cfg->task, cfg->rand_flags, cfg->num_envs, *(const mg_library *)cfg->library);
-    s->step_variant = pick_step_variant(s->caps, cfg->num_envs);
+    s->step_variant = pick_step_variant(s->caps, cfg->num_envs, cfg->task);
     s->step_blk = pick_step_blk(s->step_variant);
     err = hipMalloc((void **)&s->reset_mask, (size_t)s->S.N);
     if (err != hipSuccess) { (void)hipFree(s->pool); (void)hipFree(s->dlib); delete s; return set_err(-12, "mg_create: hipMalloc mask"); }

@@ -86,6 +86,56 @@ def test_rollout_parity(name, n, steps):
     vec.close()
 
 
+# every compiled step-kernel form, forced through the experiment switches read at mg_create
+# (MG_STEP_VARIANT: 0 = HBM state, 1/2 = compile-time constraint lists, 3 = LDS with runtime lists;
+# MG_STEP_BLK / MG_STEP_BLK0: envs per workgroup)
+KERNEL_FORMS = [
+    ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_BLK": "1"}),
+    ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_BLK": "4"}),
+    ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "8"}),
+    ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_BLK": "4"}),
+    ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "1"}),
+    ("ClusterColour-Demo-LoResStack-v0", 66, 30, {"MG_STEP_VARIANT": "3", "MG_STEP_BLK": "1"}),
+    ("ClusterColour-Demo-LoResStack-v0", 66, 30, {"MG_STEP_VARIANT": "3", "MG_STEP_BLK": "4"}),
+    ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0"}),
+    ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "8"}),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n,steps,env", KERNEL_FORMS)
+def test_step_kernel_forms(name, n, steps, env, monkeypatch):
+    """Every step-kernel form gives the oracle's trajectories (a spread of envs across workgroups)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    spec = registry.lookup(name)
+    seeds = [300 + i for i in range(n)]
+    vec = magical_amd.make_vec(name, n, seeds=seeds)
+    pick = sorted({0, 1, 3, 4, 15, 16, 17, 63, 64, n - 1})
+    orc = {i: oracle_env(spec, seeds[i]) for i in pick}
+    acts = np.random.RandomState(11).randint(0, 18, (steps, n))
+    vec.reset()
+    for i in pick:
+        orc[i].reset()
+    for t in range(steps):
+        obs, rew, done, info = vec.step(torch.as_tensor(acts[t], dtype=torch.uint8))
+        got = {k: v[pick].cpu().numpy() for k, v in obs.items()}
+        bodies, _ = vec.bodies()
+        bodies = bodies[pick].cpu().numpy()
+        for j, i in enumerate(pick):
+            o, r, d, s = orc[i].step(int(acts[t, i]))
+            if d:
+                o = orc[i].reset()
+            else:
+                b = orc[i].bodies()
+                assert np.abs(bodies[j, :len(b)] - b).max() <= POSE_TOL, f"step {t} env {i} bodies"
+            ref = oracle_obs_split(spec, o)
+            for k in got:
+                assert np.array_equal(got[k][j], ref[k]), f"step {t} env {i} obs {k}"
+    assert int(vec.errors().abs().sum().item()) == 0
+    vec.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", [c[0] for c in CONFIGS])
 def test_full_resolution_frames(name):
