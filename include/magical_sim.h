@@ -32,7 +32,7 @@ extern "C" {
 typedef struct mg_sim mg_sim;
 
 typedef struct {
-    int32_t task;              /* 0 MoveToRegion 1 MoveToCorner 2 ClusterColour 3 ClusterShape 4 MatchRegions */
+    int32_t task;              /* 0 MoveToRegion 1 MoveToCorner 2 ClusterColour 3 ClusterShape 4 MatchRegions 5 MakeLine */
     int32_t rand_flags;        /* bit 0 layout minor, 1 layout full, 2 colour, 3 shape type, 4 count, 5 dynamics */
     int32_t preproc;           /* 0 none, 1 LoRes4E, 2 LoResStack, 4 LoRes4A */
     int32_t num_envs;

@@ -358,6 +358,12 @@ __constant__ static const double CC_POSES[2][8][3] = {
      {0.867, -0.149, -2.215}, {-0.785, -0.140, -0.405}, {-0.305, -0.226, 1.341}, {0.758, -0.708, -2.140}}};
 __constant__ static const double CC_ROBOT[2][3] = {{0.71692, -0.34374, 0.83693}, {0.286, -0.202, -1.878}};
 
+// make_line.py:13-27
+__constant__ static const int ML_COLOURS[4] = {MG_COL_BLUE, MG_COL_YELLOW, MG_COL_RED, MG_COL_GREEN};
+__constant__ static const int ML_TYPES[4] = {MG_SHAPE_STAR, MG_SHAPE_CIRCLE, MG_SHAPE_STAR, MG_SHAPE_PENTAGON};
+__constant__ static const double ML_POSES[4][3] = {{0.790, -0.820, -0.721}, {-0.177, 0.383, -1.733},
+                                                   {-0.051, -0.128, 2.696}, {-0.292, -0.745, -0.159}};
+
 MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg) {
     size_t N = (size_t)S.N;
     const int f = cfg.flags;
@@ -429,6 +435,27 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             for (int i = 0; i < n; i++) { rr[i] = true; rl[i] = full ? -1.0 : JITTER_ROT_BOUND; }
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
             randomise_all(S, L, e, ents, n, rr, full ? -1.0 : JITTER_POS_BOUND, rl);
+        }
+    } else if (cfg.task == MG_TASK_MAKE_LINE) { // make_line.py:86-132
+        int nblk = 4;
+        const bool count = (f & MG_RAND_SHAPE_COUNT) != 0;
+        if (count) nblk = mt_randint(S, e, 3, 4 + 1);
+        int cols[4], types[4];
+        for (int i = 0; i < 4; i++) { cols[i] = ML_COLOURS[i]; types[i] = ML_TYPES[i]; }
+        if (f & MG_RAND_COLOUR) for (int i = 0; i < nblk; i++) cols[i] = MG_SHAPE_COLOURS[mt_randint(S, e, 0, 4)];
+        if (f & MG_RAND_SHAPE_TYPE) for (int i = 0; i < nblk; i++) types[i] = MG_SHAPE_TYPES[mt_randint(S, e, 0, 4)];
+        for (int i = 0; i < nblk; i++) { // with a random count every block starts at the first default pose
+            const int k = count ? 0 : i;
+            inst_block(S, L, e, B, types[i], cols[i], 0, ML_POSES[k][0], ML_POSES[k][1], ML_POSES[k][2], star_groups);
+        }
+        inst_robot(S, L, e, B, 0.702, -0.255, 0.347);
+        if (any_layout) {
+            ents[0] = 1 + nblk; // robot, then the blocks
+            for (int i = 0; i < nblk; i++) ents[1 + i] = 1 + i;
+            n = nblk + 1;
+            for (int i = 0; i < n; i++) { rr[i] = true; rl[i] = minor ? JITTER_ROT_BOUND : -1.0; }
+            S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
+            randomise_all(S, L, e, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl);
         }
     } else { // MatchRegions
         int target = MG_COL_GREEN;

@@ -26,6 +26,42 @@ MG_DEV double poly_point_query(const ShapeW &sh, V2 p) {
     return dist - sh.r;
 }
 
+#define MG_MAX_LINE 8
+// make_line.py:33-74 longest_line in the reference's numpy arithmetic (oracle/scene.c o_longest_line):
+// norm of one 2-vector = sqrt(ddot) = sqrt(fma(y, y, x*x)); offs @ unit (gemv) = fma(x, ux, y*uy);
+// norm(axis=1) = sqrt(x*x + y*y)
+MG_DEV int longest_line(const double *px, const double *py, int n, double inlier_dist, double max_sep) {
+    int best = n < 1 ? n : 1;
+    for (int i = 0; i < n - 1; i++)
+        for (int j = i + 1; j < n; j++) {
+            double inl[MG_MAX_LINE];
+            const double jx = px[j] - px[i], jy = py[j] - py[i];
+            const double nrm = sqrt(__fma_rn(jy, jy, jx * jx));
+            const double ux = jx / nrm, uy = jy / nrm;
+            int ni = 0;
+            for (int k = 0; k < n; k++) {
+                const double ox = px[k] - px[i], oy = py[k] - py[i];
+                const double proj = __fma_rn(ox, ux, oy * uy);
+                const double dx = ox - proj * ux, dy = oy - proj * uy;
+                if (sqrt(dx * dx + dy * dy) <= inlier_dist) inl[ni++] = proj;
+            }
+            if (ni <= best) continue;
+            for (int a = 1; a < ni; a++) {
+                const double v = inl[a];
+                int b = a - 1;
+                while (b >= 0 && inl[b] > v) { inl[b + 1] = inl[b]; b--; }
+                inl[b + 1] = v;
+            }
+            int run = 0, max_run = 0;
+            for (int k = 0; k + 1 < ni; k++) {
+                if (fabs(inl[k + 1] - inl[k]) <= max_sep) { run++; max_run = run > max_run ? run : max_run; }
+                else run = 0;
+            }
+            best = max_run + 1 > best ? max_run + 1 : best;
+        }
+    return best;
+}
+
 MG_DEV double score_env(const MGState &S, const mg_library *L, int e, int task) {
     int rb = S.robot_body0[e];
     V2 rp = v2(AT(S.bpx, rb), AT(S.bpy, rb));
@@ -87,6 +123,19 @@ MG_DEV double score_env(const MGState &S, const mg_library *L, int e, int task) 
         double frac = (double)n_correct / (n_blocks > 1 ? n_blocks : 1);
         double v = frac - 0.75;
         return (v > 0 ? v : 0) / (1 - 0.75);
+    }
+    if (task == MG_TASK_MAKE_LINE) { // make_line.py:140-152
+        double px[MG_MAX_LINE], py[MG_MAX_LINE];
+        int n = 0;
+        for (int i = 0; i < nents && n < MG_MAX_LINE; i++) {
+            if (AT(S.ekind, i) != MG_ENT_BLOCK) continue;
+            const int b = AT(S.ebody0, i);
+            px[n] = AT(S.bpx, b); py[n] = AT(S.bpy, b); n++;
+        }
+        const double rad = L->robot_radius * 0.6; // BaseEnv.SHAPE_RAD
+        const int line_len = longest_line(px, py, n, rad * 1.5, rad * 3.5);
+        const int min_len = n - 2 > 2 ? n - 2 : 2, d = line_len - min_len;
+        return (double)(d > 0 ? d : 0) / (double)(n - min_len);
     }
     // MatchRegions
     int ge = S.goal_ent[e];

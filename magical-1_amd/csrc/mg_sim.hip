@@ -158,6 +158,7 @@ static StepCaps step_caps(int task, int flags, int n_envs, const mg_library &lib
     case MG_TASK_MOVE_TO_CORNER: nblk = 1; star_ok = (flags & MG_RAND_SHAPE_TYPE) != 0; break;
     case MG_TASK_CLUSTER_COLOUR:
     case MG_TASK_CLUSTER_SHAPE: nblk = (flags & MG_RAND_SHAPE_COUNT) ? 10 : 8; break;
+    case MG_TASK_MAKE_LINE: nblk = 4; break;
     default: nblk = (flags & MG_RAND_SHAPE_COUNT) ? 8 : 5; break;
     }
     const int per_blk = star_ok ? lib.block_nshapes[MG_SHAPE_STAR] : 1;
@@ -234,7 +235,7 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     if (cfg->library_size != (int64_t)sizeof(mg_library))
         return set_err(-22, "mg_create: library_size mismatch (expected " + std::to_string(sizeof(mg_library)) + ")");
     if (cfg->num_envs <= 0) return set_err(-22, "mg_create: num_envs must be positive");
-    if (cfg->task < 0 || cfg->task > 4) return set_err(-22, "mg_create: unknown task");
+    if (cfg->task < 0 || cfg->task > MG_TASK_MAKE_LINE) return set_err(-22, "mg_create: unknown task");
     if (cfg->preproc != MG_PREPROC_LORES4E && cfg->preproc != MG_PREPROC_LORESSTACK &&
         cfg->preproc != MG_PREPROC_LORES4A && cfg->preproc != MG_PREPROC_LORES3EA && cfg->preproc != MG_PREPROC_NONE)
         return set_err(-95, "mg_create: preprocessor not supported by the GPU path");

@@ -24,10 +24,12 @@ def make(env_name, device="cuda:0", seed=None):
     return MagicalEnv(env_name, device=device, seed=seed)
 
 
-def make_vec(env_name, num_envs, device="cuda:0", seeds=None, base_seed=0, auto_reset=True):
-    """num_envs instances of env_name on one GPU (batched, auto-resetting)."""
+def make_vec(env_name, num_envs, device="cuda:0", seeds=None, base_seed=0, auto_reset=True, max_episode_steps=None):
+    """num_envs instances of env_name on one GPU (batched, auto-resetting).  max_episode_steps
+    overrides the registered episode length (gym.make(..., max_episode_steps=...))."""
     from .envs import VecMagicalEnv
-    return VecMagicalEnv(env_name, num_envs, device=device, seeds=seeds, base_seed=base_seed, auto_reset=auto_reset)
+    return VecMagicalEnv(env_name, num_envs, device=device, seeds=seeds, base_seed=base_seed, auto_reset=auto_reset,
+                         max_episode_steps=max_episode_steps)
 
 
 def register_envs():

@@ -50,7 +50,8 @@ def observation_space(spec):
 class VecMagicalEnv:
     """Batched MAGICAL env on one MI355X (C ABI: include/magical_sim.h)."""
 
-    def __init__(self, env_name, num_envs, device="cuda:0", seeds=None, base_seed=0, auto_reset=True):
+    def __init__(self, env_name, num_envs, device="cuda:0", seeds=None, base_seed=0, auto_reset=True,
+                 max_episode_steps=None):
         self.spec = registry.lookup(env_name)
         if not self.spec.gpu_supported:
             raise NotImplementedError(f"{env_name}: task not on the GPU hot path yet")
@@ -66,7 +67,8 @@ class VecMagicalEnv:
         cfg.preproc = gpu_pp
         cfg.num_envs = self.num_envs
         cfg.device = self.device.index or 0
-        cfg.max_episode_steps = self.spec.max_episode_steps
+        self.max_episode_steps = int(max_episode_steps or self.spec.max_episode_steps)
+        cfg.max_episode_steps = self.max_episode_steps
         cfg.base_seed = base_seed
         cfg.auto_reset = 1 if auto_reset else 0
         if seeds is not None:

@@ -14,7 +14,8 @@ from typing import Optional
 # rand flag bits (include/magical_sim.h, mg_common.h)
 LAYOUT_MINOR, LAYOUT_FULL, COLOUR, SHAPE_TYPE, SHAPE_COUNT, DYNAMICS = 1, 2, 4, 8, 16, 32
 
-TASK_IDS = {"MoveToRegion": 0, "MoveToCorner": 1, "ClusterColour": 2, "ClusterShape": 3, "MatchRegions": 4}
+TASK_IDS = {"MoveToRegion": 0, "MoveToCorner": 1, "ClusterColour": 2, "ClusterShape": 3, "MatchRegions": 4,
+            "MakeLine": 5}
 GPU_TASKS = set(TASK_IDS)
 
 PREPROCESSORS = collections.OrderedDict([

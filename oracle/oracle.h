@@ -43,7 +43,7 @@ typedef struct { double x, y; } vec2;
 
 /* ---- tasks / variants / preprocessors (benchmarks/__init__.py:269-307,427-1102) */
 enum { TASK_MOVE_TO_REGION = 0, TASK_MOVE_TO_CORNER = 1, TASK_CLUSTER_COLOUR = 2,
-       TASK_CLUSTER_SHAPE = 3, TASK_MATCH_REGIONS = 4 };
+       TASK_CLUSTER_SHAPE = 3, TASK_MATCH_REGIONS = 4, TASK_MAKE_LINE = 5 };
 enum { RAND_LAYOUT_MINOR = 1, RAND_LAYOUT_FULL = 2, RAND_COLOUR = 4, RAND_SHAPE_TYPE = 8,
        RAND_SHAPE_COUNT = 16, RAND_DYNAMICS = 32 };
 enum { PREPROC_NONE = 0, PREPROC_LORES4E = 1, PREPROC_LORESSTACK = 2, PREPROC_LORES3EA = 3,

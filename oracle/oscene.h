@@ -62,6 +62,7 @@ void oscene_reset(OEnv *e);
 void oscene_robot_update(OEnv *e);
 void oscene_set_action(OEnv *e, int action);
 double oscene_score(OEnv *e);
+int o_longest_line(const double *px, const double *py, int n, double inlier_dist, double max_sep);
 void oscene_pre_draw(OEnv *e);
 /* raster.c */
 void oraster_render(const OEnv *e, int ego, uint8_t *frame384);

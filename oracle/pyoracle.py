@@ -14,7 +14,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "libmg_oracle.so")
 
-TASKS = {"MoveToRegion": 0, "MoveToCorner": 1, "ClusterColour": 2, "ClusterShape": 3, "MatchRegions": 4}
+TASKS = {"MoveToRegion": 0, "MoveToCorner": 1, "ClusterColour": 2, "ClusterShape": 3, "MatchRegions": 4,
+         "MakeLine": 5}
 PREPROCS = {None: 0, "LoRes4E": 1, "LoResStack": 2, "LoRes3EA": 3, "LoRes4A": 4, "LoResCHW4E": 5, "LoResCHW4A": 5}
 
 _lib = None
@@ -49,6 +50,7 @@ def lib():
         L.o_mt_double.restype = d; L.o_mt_double.argtypes = [vp]
         L.o_mt_uniform.restype = d; L.o_mt_uniform.argtypes = [vp, d, d]
         L.o_mt_randint.restype = ctypes.c_int64; L.o_mt_randint.argtypes = [vp, ctypes.c_int64, ctypes.c_int64]
+        L.o_longest_line.restype = i; L.o_longest_line.argtypes = [vp, vp, i, d, d]
         L.o_mt_interval.restype = ctypes.c_uint64; L.o_mt_interval.argtypes = [vp, ctypes.c_uint64]
         L.o_convex_hull.restype = i; L.o_convex_hull.argtypes = [i, vp, vp, vp, d]
         L.o_moment_for_poly.restype = d

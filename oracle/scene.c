@@ -861,6 +861,41 @@ static void reset_match_regions(OEnv *e) {
     }
 }
 
+/* make_line.py:13-27 defaults, :86-132 on_reset */
+static const int ML_COLOURS[4] = {COL_BLUE, COL_YELLOW, COL_RED, COL_GREEN};
+static const int ML_TYPES[4] = {SHAPE_STAR, SHAPE_CIRCLE, SHAPE_STAR, SHAPE_PENTAGON};
+static const double ML_POSES[4][3] = {{0.790, -0.820, -0.721}, {-0.177, 0.383, -1.733},
+                                      {-0.051, -0.128, 2.696}, {-0.292, -0.745, -0.159}};
+static const double ML_ROBOT[3] = {0.702, -0.255, 0.347};
+
+static void reset_make_line(OEnv *e) {
+    int f = e->flags;
+    int n = 4;
+    double poses[4][3];
+    memcpy(poses, ML_POSES, sizeof(poses));
+    if (f & RAND_SHAPE_COUNT) { /* rng.randint(MIN_BLOCKS, MAX_BLOCKS + 1); block_poses[:1] * n */
+        n = (int)o_mt_randint(&e->rng, 3, 4 + 1);
+        for (int i = 0; i < n; i++) memcpy(poses[i], ML_POSES[0], sizeof(poses[i]));
+    }
+    int cols[4], types[4];
+    memcpy(cols, ML_COLOURS, sizeof(cols));
+    memcpy(types, ML_TYPES, sizeof(types));
+    /* rng.choice(list, size=n) = randint(0, len, size=n) */
+    if (f & RAND_COLOUR) for (int i = 0; i < n; i++) cols[i] = SHAPE_COLOURS[o_mt_randint(&e->rng, 0, 4)];
+    if (f & RAND_SHAPE_TYPE) for (int i = 0; i < n; i++) types[i] = SHAPE_TYPES[o_mt_randint(&e->rng, 0, 4)];
+    int first_block = e->nents;
+    for (int i = 0; i < n; i++) add_block(e, types[i], cols[i], v2(poses[i][0], poses[i][1]), poses[i][2], 0);
+    add_robot(e, v2(ML_ROBOT[0], ML_ROBOT[1]), ML_ROBOT[2]);
+    if (f & (RAND_LAYOUT_MINOR | RAND_LAYOUT_FULL)) { /* all_ents = (robot, *blocks), rand_rot everywhere */
+        int ents[8], rr[8]; double rl[8];
+        int minor = (f & RAND_LAYOUT_MINOR) != 0;
+        ents[0] = e->robot;
+        for (int i = 0; i < n; i++) ents[1 + i] = first_block + i;
+        for (int i = 0; i <= n; i++) { rr[i] = 1; rl[i] = minor ? JITTER_ROT_BOUND : -1; }
+        randomise_all_poses(e, ents, n + 1, rr, minor ? JITTER_POS_BOUND : -1, rl);
+    }
+}
+
 void oscene_reset(OEnv *e) {
     e->episode_steps = 0;
     e->nents = 0; e->ngeoms = 0; e->nxf = 0; e->robot = -1; e->goal = -1; e->star_groups = 0;
@@ -878,6 +913,7 @@ void oscene_reset(OEnv *e) {
     case TASK_CLUSTER_COLOUR: reset_cluster(e, 0); break;
     case TASK_CLUSTER_SHAPE: reset_cluster(e, 1); break;
     case TASK_MATCH_REGIONS: reset_match_regions(e); break;
+    case TASK_MAKE_LINE: reset_make_line(e); break;
     }
     /* Robot.__init__ control state (entities.py:219-228, 287) */
     e->rel_turn = 0.0;
@@ -1059,6 +1095,56 @@ static double score_match_regions(OEnv *e) {
     return frac * (1 - contamination);
 }
 
+/* make_line.py:33-74 longest_line, in this image's numpy arithmetic: np.linalg.norm of one
+ * 2-vector = sqrt(ddot) = sqrt(fma(y, y, x * x)); offs @ unit[:, None] (OpenBLAS gemv) =
+ * fma(x, ux, y * uy); np.linalg.norm(..., axis=1) = sqrt(x * x + y * y) */
+int o_longest_line(const double *px, const double *py, int n, double inlier_dist, double max_sep) {
+    int best = n < 1 ? n : 1;
+    for (int i = 0; i < n - 1; i++)
+        for (int j = i + 1; j < n; j++) {
+            double ox[16], oy[16], proj[16], inl[16];
+            for (int k = 0; k < n; k++) { ox[k] = px[k] - px[i]; oy[k] = py[k] - py[i]; }
+            const double nrm = sqrt(fma(oy[j], oy[j], ox[j] * ox[j]));
+            const double ux = ox[j] / nrm, uy = oy[j] / nrm;
+            int ni = 0;
+            for (int k = 0; k < n; k++) {
+                proj[k] = fma(ox[k], ux, oy[k] * uy);
+                const double dx = ox[k] - proj[k] * ux, dy = oy[k] - proj[k] * uy;
+                if (sqrt(dx * dx + dy * dy) <= inlier_dist) inl[ni++] = proj[k];
+            }
+            if (ni <= best) continue;
+            for (int a = 1; a < ni; a++) { /* sort */
+                double v = inl[a]; int b = a - 1;
+                while (b >= 0 && inl[b] > v) { inl[b + 1] = inl[b]; b--; }
+                inl[b + 1] = v;
+            }
+            int run = 0, max_run = 0; /* longest run of separations <= max_sep */
+            for (int k = 0; k + 1 < ni; k++) {
+                if (fabs(inl[k + 1] - inl[k]) <= max_sep) { run++; if (run > max_run) max_run = run; }
+                else run = 0;
+            }
+            if (max_run + 1 > best) best = max_run + 1;
+        }
+    return best;
+}
+
+/* make_line.py:140-152 */
+static double score_make_line(OEnv *e) {
+    double px[16], py[16];
+    int n = 0;
+    for (int i = 0; i < e->nents; i++) {
+        OEntity *en = &e->ents[i];
+        if (en->kind != ENT_BLOCK) continue;
+        vec2 p = e->space.bodies[en->body0].p;
+        px[n] = p.x; py[n] = p.y; n++;
+    }
+    const double rad = shape_rad();
+    int line_len = o_longest_line(px, py, n, rad * 1.5, rad * 3.5);
+    int min_len = n - 2 > 2 ? n - 2 : 2;
+    int d = line_len - min_len;
+    return (double)(d > 0 ? d : 0) / (double)(n - min_len);
+}
+
 double oscene_score(OEnv *e) {
     switch (e->task) {
     case TASK_MOVE_TO_REGION: return score_move_to_region(e);
@@ -1066,6 +1152,7 @@ double oscene_score(OEnv *e) {
     case TASK_CLUSTER_COLOUR: return score_cluster(e, 0);
     case TASK_CLUSTER_SHAPE: return score_cluster(e, 1);
     case TASK_MATCH_REGIONS: return score_match_regions(e);
+    case TASK_MAKE_LINE: return score_make_line(e);
     }
     return 0.0;
 }

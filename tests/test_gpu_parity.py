@@ -20,6 +20,12 @@ CONFIGS = [
     ("ClusterColour-Demo-LoResStack-v0", 3, 60),
     ("MatchRegions-TestAll-LoRes4E-v0", 4, 130),
 ]
+# SURVEY.md 8(f) F1 tasks: full episodes (scores at done) for the Demo and the most random variant
+TASK_CONFIGS = [
+    ("MakeLine-Demo-LoRes4E-v0", 3, 185),
+    ("MakeLine-TestAll-LoRes4E-v0", 4, 185),
+    ("MakeLine-TestCountPlus-LoResStack-v0", 3, 40),
+]
 # the other observation preprocessors (benchmarks/__init__.py:51-190): same rollout check
 PREPROC_CONFIGS = [
     ("MoveToRegion-Demo-LoRes3EA-v0", 4, 45),
@@ -46,7 +52,7 @@ def oracle_env(spec, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,n,steps", CONFIGS + PREPROC_CONFIGS)
+@pytest.mark.parametrize("name,n,steps", CONFIGS + PREPROC_CONFIGS + TASK_CONFIGS)
 def test_rollout_parity(name, n, steps):
     spec = registry.lookup(name)
     seeds = [1000 + i for i in range(n)]
@@ -134,6 +140,41 @@ def test_step_kernel_forms(name, n, steps, env, monkeypatch):
                 assert np.array_equal(got[k][j], ref[k]), f"step {t} env {i} obs {k}"
     assert int(vec.errors().abs().sum().item()) == 0
     vec.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["MakeLine-TestLayout-v0", "MakeLine-TestCountPlus-v0", "MatchRegions-TestLayout-v0",
+                                  "ClusterColour-TestLayout-v0", "ClusterShape-TestLayout-v0",
+                                  "MoveToRegion-TestLayout-v0", "MoveToCorner-TestAll-v0"])
+def test_scores_on_random_layouts(name):
+    """Episode length 1: every env is scored on its randomised initial layout (plus one step), so
+    the scorers see many non-trivial layouts; GPU eval_score == oracle for all of them."""
+    spec = registry.lookup(name)
+    n = 512
+    seeds = [5000 + i for i in range(n)]
+    vec = magical_amd.make_vec(name, n, seeds=seeds, max_episode_steps=1, auto_reset=False)
+    vec.reset()
+    acts = np.random.RandomState(2).randint(0, 18, n)
+    _, rew, done, info = vec.step(torch.as_tensor(acts, dtype=torch.uint8))
+    got = info["eval_score"].cpu().numpy()
+    errs = vec.errors().cpu().numpy()
+    assert bool(done.all())
+    ref = np.zeros(n)
+    placement = np.zeros(n, dtype=bool)
+    for i in range(n):
+        o = po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, 1, seed=seeds[i])
+        try:
+            o.reset()
+        except po.PlacementError:  # geom.py:335-336 (e.g. MoveToCorner robot drawn next to a corner)
+            placement[i] = True
+            continue
+        ref[i] = o.step(int(acts[i]))[3]
+    assert np.array_equal((errs & 2) != 0, placement)
+    ok = ~placement
+    assert np.array_equal(got[ok], ref[ok]), np.nonzero(got[ok] != ref[ok])
+    assert int(np.abs(errs & ~2).sum()) == 0
+    vec.close()
+    print(name, "non-zero scores:", int((ref > 0).sum()), "of", n)
 
 
 @pytest.mark.gpu
