@@ -32,7 +32,7 @@ extern "C" {
 typedef struct mg_sim mg_sim;
 
 typedef struct {
-    int32_t task;              /* 0 MoveToRegion 1 MoveToCorner 2 ClusterColour 3 ClusterShape 4 MatchRegions 5 MakeLine */
+    int32_t task;              /* 0 MoveToRegion 1 MoveToCorner 2 ClusterColour 3 ClusterShape 4 MatchRegions 5 MakeLine 6 FindDupe 7 FixColour */
     int32_t rand_flags;        /* bit 0 layout minor, 1 layout full, 2 colour, 3 shape type, 4 count, 5 dynamics */
     int32_t preproc;           /* 0 none, 1 LoRes4E, 2 LoResStack, 4 LoRes4A */
     int32_t num_envs;
@@ -71,6 +71,9 @@ int mg_render_full(mg_sim *sim, uint8_t *out_dev, void *stream);
 /* parity dumps: per env per body slot (px, py, angle, vx, vy, w): device f64[N,16,6];
  * counts: device i32[N,4] = (bodies, shapes, constraints, active arbiters) */
 int mg_get_bodies(mg_sim *sim, double *out_dev, int32_t *counts_dev, void *stream);
+/* set body `body` of env `env` to (x, y, angle) like pymunk's Body.position / Body.angle setters
+ * (geom.py:362-384 pm_shift_bodies applies them); for parity tests that place blocks before a step */
+int mg_set_body_pose(mg_sim *sim, int env, int body, double x, double y, double angle, void *stream);
 /* per-env error flags (table overflow, placement failure, raster assumption): device i32[N] */
 int mg_get_errors(mg_sim *sim, int32_t *out_dev, void *stream);
 /* re-seed env RNGs (env.seed): host u32[num_envs] */

@@ -26,7 +26,8 @@
 
 // tasks / rand flags / preprocessors (mirror benchmarks/__init__.py:269-307, 427-1102)
 enum { MG_TASK_MOVE_TO_REGION = 0, MG_TASK_MOVE_TO_CORNER = 1, MG_TASK_CLUSTER_COLOUR = 2,
-       MG_TASK_CLUSTER_SHAPE = 3, MG_TASK_MATCH_REGIONS = 4, MG_TASK_MAKE_LINE = 5 };
+       MG_TASK_CLUSTER_SHAPE = 3, MG_TASK_MATCH_REGIONS = 4, MG_TASK_MAKE_LINE = 5,
+       MG_TASK_FIND_DUPE = 6, MG_TASK_FIX_COLOUR = 7 };
 enum { MG_RAND_LAYOUT_MINOR = 1, MG_RAND_LAYOUT_FULL = 2, MG_RAND_COLOUR = 4, MG_RAND_SHAPE_TYPE = 8,
        MG_RAND_SHAPE_COUNT = 16, MG_RAND_DYNAMICS = 32 };
 enum { MG_PREPROC_NONE = 0, MG_PREPROC_LORES4E = 1, MG_PREPROC_LORESSTACK = 2, MG_PREPROC_LORES3EA = 3,

@@ -361,7 +361,7 @@ MG_DEV void entity_xforms(const MGState &S, int e, int ent, double (*xf)[9]) {
         int b = AT(S.ebody0, ent);
         mg_transform_tr(AT(S.bpx, b), AT(S.bpy, b), AT(S.ba, b), xf[MG_XF_MAIN]);
     } else if (kind == MG_ENT_GOAL) {
-        mg_transform_tr(S.gpx[e], S.gpy[e], 0.0, xf[MG_XF_MAIN]);
+        mg_transform_tr(AT(S.ex, ent), AT(S.ey, ent), 0.0, xf[MG_XF_MAIN]);
     }
 }
 

@@ -167,8 +167,10 @@ MG_DEV void add_block(const MGState &S, const mg_library *L, int e, Builder &B, 
 }
 
 // ---- shape queries (cpSpaceShapeQuery semantics, sensors reported) --------
-MG_DEV bool query_hits(const MGState &S, const mg_library *L, int e, const ShapeW &A, int self_k, int group, bool has_goal,
-                       bool self_is_goal) {
+// A is entity self_ent's shape (or goal); ign = bit mask of entities whose shapes are ignored
+// (pm_randomise_pose ignore_shapes, geom.py:116-264).
+MG_DEV bool query_hits(const MGState &S, const mg_library *L, int e, const ShapeW &A, int self_k, int group, int self_ent,
+                       uint32_t ign) {
     for (int w = 0; w < 4; w++) {
         ShapeW W;
         load_wall(w, W);
@@ -177,21 +179,19 @@ MG_DEV bool query_hits(const MGState &S, const mg_library *L, int e, const Shape
         collide(A, W, info);
         if (info.count) return true;
     }
-    if (has_goal && !self_is_goal) {
-        int ge = S.goal_ent[e];
-        if (AT(S.eshape0, ge) != 0) { // goal enabled (categories != 0)
-            ShapeW G;
-            load_goal(S.gpx[e], S.gpy[e], AT(S.ew, ge), AT(S.eh, ge), 0, G);
-            if (bb_intersects(A, G)) {
-                Collision info;
-                collide(A, G, info);
-                if (info.count) return true;
-            }
-        }
+    const int nents = S.nents[e];
+    for (int g = 0; g < nents; g++) { // goal sensors (enabled: categories != 0)
+        if (AT(S.ekind, g) != MG_ENT_GOAL || g == self_ent || ((ign >> g) & 1u) || AT(S.eshape0, g) == 0) continue;
+        ShapeW G;
+        load_goal(AT(S.ex, g), AT(S.ey, g), AT(S.ew, g), AT(S.eh, g), 0, G);
+        if (!bb_intersects(A, G)) continue;
+        Collision info;
+        collide(A, G, info);
+        if (info.count) return true;
     }
     int ns = S.nshapes[e];
     for (int j = 0; j < ns; j++) {
-        if (j == self_k || !AT(S.scat, j)) continue;
+        if (j == self_k || !AT(S.scat, j) || ((ign >> AT(S.sent, j)) & 1u)) continue;
         int gj = AT(S.sgroup, j);
         if (group != 0 && group == gj) continue;
         ShapeW O;
@@ -213,10 +213,10 @@ MG_DEV void ent_set_enabled(const MGState &S, int e, int ent, int on) {
 // pm_shift_bodies (geom.py:362-384)
 MG_DEV void shift_entity(const MGState &S, int e, int ent, V2 pos, double ang) {
     if (AT(S.ekind, ent) == MG_ENT_GOAL) {
-        V2 root = v2(S.gpx[e], S.gpy[e]);
-        V2 d = v2(S.gpx[e] - root.x, S.gpy[e] - root.y);
+        V2 root = v2(AT(S.ex, ent), AT(S.ey, ent));
+        V2 d = v2(AT(S.ex, ent) - root.x, AT(S.ey, ent) - root.y);
         V2 r = rotated(d, ang - 0.0);
-        S.gpx[e] = pos.x + r.x; S.gpy[e] = pos.y + r.y;
+        AT(S.ex, ent) = pos.x + r.x; AT(S.ey, ent) = pos.y + r.y;
         return;
     }
     int b0 = AT(S.ebody0, ent);
@@ -236,29 +236,28 @@ MG_DEV void shift_entity(const MGState &S, int e, int ent, V2 pos, double ang) {
     }
 }
 
-MG_DEV bool entity_collides(const MGState &S, const mg_library *L, int e, int ent) {
-    bool has_goal = S.goal_ent[e] >= 0;
+MG_DEV bool entity_collides(const MGState &S, const mg_library *L, int e, int ent, uint32_t ign) {
     if (AT(S.ekind, ent) == MG_ENT_GOAL) {
         ShapeW G;
-        load_goal(S.gpx[e], S.gpy[e], AT(S.ew, ent), AT(S.eh, ent), 0, G);
-        return query_hits(S, L, e, G, -1, 0, has_goal, true);
+        load_goal(AT(S.ex, ent), AT(S.ey, ent), AT(S.ew, ent), AT(S.eh, ent), 0, G);
+        return query_hits(S, L, e, G, -1, 0, ent, ign);
     }
     int s0 = AT(S.eshape0, ent), n = AT(S.enshapes, ent);
     for (int k = s0; k < s0 + n; k++) {
         ShapeW A;
         load_shape(S, L, e, k, 0, A);
-        if (query_hits(S, L, e, A, k, AT(S.sgroup, k), has_goal, false)) return true;
+        if (query_hits(S, L, e, A, k, AT(S.sgroup, k), ent, ign)) return true;
     }
     return false;
 }
 
 // pm_randomise_pose (geom.py:116-264); pos_limit / rot_limit < 0 mean None
 MG_DEV int randomise_pose(const MGState &S, const mg_library *L, int e, int ent, bool rand_rot, double pos_limit,
-                          double rot_limit) {
+                          double rot_limit, uint32_t ign = 0u) {
     bool goal = AT(S.ekind, ent) == MG_ENT_GOAL;
     int b0 = goal ? -1 : AT(S.ebody0, ent);
     double orig_a = goal ? 0.0 : AT(S.ba, b0);
-    V2 orig_p = goal ? v2(S.gpx[e], S.gpy[e]) : v2(AT(S.bpx, b0), AT(S.bpy, b0));
+    V2 orig_p = goal ? v2(AT(S.ex, ent), AT(S.ey, ent)) : v2(AT(S.bpx, b0), AT(S.bpy, b0));
     double xlo = -1, xhi = 1, ylo = -1, yhi = 1;
     if (pos_limit >= 0) {
         xlo = fmax(-1.0, orig_p.x - pos_limit); xhi = fmin(1.0, orig_p.x + pos_limit);
@@ -271,20 +270,20 @@ MG_DEV int randomise_pose(const MGState &S, const mg_library *L, int e, int ent,
         double y = mt_uniform(S, e, ylo, yhi);
         double a = rand_rot ? mt_uniform(S, e, rmin, rmax) : orig_a;
         shift_entity(S, e, ent, v2(x, y), a);
-        if (!entity_collides(S, L, e, ent)) return 0;
+        if (!entity_collides(S, L, e, ent, ign)) return 0;
     }
     shift_entity(S, e, ent, orig_p, orig_a);
     return -1;
 }
 
 MG_DEV void randomise_all(const MGState &S, const mg_library *L, int e, const int *ents, int n, const bool *rand_rot,
-                          double pos_limit, const double *rot_limits) {
+                          double pos_limit, const double *rot_limits, uint32_t ign = 0u) {
     for (int retry = 0; retry < 10; retry++) {
         for (int k = 0; k < n; k++) ent_set_enabled(S, e, ents[k], 0);
         bool failed = false;
         for (int k = 0; k < n && !failed; k++) {
             ent_set_enabled(S, e, ents[k], 1);
-            if (randomise_pose(S, L, e, ents[k], rand_rot[k], pos_limit, rot_limits[k]) != 0) failed = true;
+            if (randomise_pose(S, L, e, ents[k], rand_rot[k], pos_limit, rot_limits[k], ign) != 0) failed = true;
         }
         if (!failed) return;
     }
@@ -323,7 +322,7 @@ MG_DEV void inst_goal(const MGState &S, int e, Builder &B, double x, double y, d
     int ent = new_entity(S, e, MG_ENT_GOAL, 0, colour, 0, x, y, 0.0);
     AT(S.eh, ent) = h; AT(S.ew, ent) = w;
     AT(S.eshape0, ent) = 1; // enabled flag for goals
-    S.gpx[e] = x + w / 2; S.gpy[e] = y - h / 2;
+    AT(S.ex, ent) = x + w / 2; AT(S.ey, ent) = y - h / 2; // the sensor body's position
     S.goal_ent[e] = ent;
     B.hash++;
 }
@@ -332,8 +331,9 @@ MG_DEV void inst_goal(const MGState &S, int e, Builder &B, double x, double y, d
 #define JITTER_ROT_BOUND (0.05 * 3.141592653589793)
 #define JITTER_TARGET_BOUND (0.05 * (0.8 - 0.5) / 2)
 
-MG_DEV void randomise_hw(const MGState &S, int e, double ch, double cw, double linf, double &h, double &w) {
-    double lo0 = 0.5, lo1 = 0.5, hi0 = 0.8, hi1 = 0.8;
+MG_DEV void randomise_hw(const MGState &S, int e, double ch, double cw, double linf, double &h, double &w,
+                         double mn = 0.5, double mx = 0.8) { // RAND_GOAL_MIN/MAX_SIZE by default
+    double lo0 = mn, lo1 = mn, hi0 = mx, hi1 = mx;
     if (linf >= 0) {
         lo0 = fmax(lo0, ch - linf); lo1 = fmax(lo1, cw - linf);
         hi0 = fmin(hi0, ch + linf); hi1 = fmin(hi1, cw + linf);
@@ -363,6 +363,23 @@ __constant__ static const int ML_COLOURS[4] = {MG_COL_BLUE, MG_COL_YELLOW, MG_CO
 __constant__ static const int ML_TYPES[4] = {MG_SHAPE_STAR, MG_SHAPE_CIRCLE, MG_SHAPE_STAR, MG_SHAPE_PENTAGON};
 __constant__ static const double ML_POSES[4][3] = {{0.790, -0.820, -0.721}, {-0.177, 0.383, -1.733},
                                                    {-0.051, -0.128, 2.696}, {-0.292, -0.745, -0.159}};
+
+// find_dupe.py:7-37
+__constant__ static const int FD_OUT_TYPES[6] = {MG_SHAPE_PENTAGON, MG_SHAPE_CIRCLE, MG_SHAPE_CIRCLE,
+                                                 MG_SHAPE_SQUARE, MG_SHAPE_STAR, MG_SHAPE_PENTAGON};
+__constant__ static const int FD_OUT_COLOURS[6] = {MG_COL_GREEN, MG_COL_RED, MG_COL_RED, MG_COL_YELLOW, MG_COL_BLUE,
+                                                   MG_COL_YELLOW};
+__constant__ static const double FD_OUT_POSES[6][3] = {{-0.066751, 0.7552, -2.9266}, {-0.05195, 0.31468, 1.5418},
+                                                       {0.57528, -0.46865, -2.2141},  {0.40594, -0.74977, 0.24582},
+                                                       {0.45254, 0.3681, -1.0834},    {0.76849, -0.10652, 0.10028}};
+// fix_colour.py:12-41
+__constant__ static const int FC_BLOCK_COLOURS[3] = {MG_COL_GREEN, MG_COL_GREEN, MG_COL_BLUE};
+__constant__ static const int FC_BLOCK_TYPES[3] = {MG_SHAPE_PENTAGON, MG_SHAPE_SQUARE, MG_SHAPE_PENTAGON};
+__constant__ static const double FC_BLOCK_POSES[3][3] = {{0.289, 0.030, 0.307}, {0.133, -0.561, 1.699},
+                                                         {-0.336, 0.000, -1.529}};
+__constant__ static const double FC_REGIONS[3][4] = {{-0.032, 0.348, 0.427, 0.468}, {0.019, -0.391, 0.460, 0.458},
+                                                     {-0.681, 0.196, 0.498, 0.418}};
+__constant__ static const int FC_REGION_COLOURS[3] = {MG_COL_GREEN, MG_COL_GREEN, MG_COL_RED};
 
 MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg) {
     size_t N = (size_t)S.N;
@@ -456,6 +473,104 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             for (int i = 0; i < n; i++) { rr[i] = true; rl[i] = minor ? JITTER_ROT_BOUND : -1.0; }
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
             randomise_all(S, L, e, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl);
+        }
+    } else if (cfg.task == MG_TASK_FIND_DUPE) { // find_dupe.py:62-199
+        int qcol = MG_COL_YELLOW, qtype = MG_SHAPE_PENTAGON, cols[6], types[6];
+        for (int i = 0; i < 6; i++) { cols[i] = FD_OUT_COLOURS[i]; types[i] = FD_OUT_TYPES[i]; }
+        const bool count = (f & MG_RAND_SHAPE_COUNT) != 0;
+        const int n_out = count ? mt_randint(S, e, 1, 5 + 1) + 1 : 6, nd = n_out - 1;
+        if (f & MG_RAND_COLOUR) {
+            qcol = MG_SHAPE_COLOURS[mt_randint(S, e, 0, 4)];
+            for (int i = 0; i < nd; i++) cols[i] = MG_SHAPE_COLOURS[mt_randint(S, e, 0, 4)];
+            cols[nd] = qcol;
+        }
+        if (f & MG_RAND_SHAPE_TYPE) {
+            qtype = MG_SHAPE_TYPES[mt_randint(S, e, 0, 4)];
+            for (int i = 0; i < nd; i++) types[i] = MG_SHAPE_TYPES[mt_randint(S, e, 0, 4)];
+            types[nd] = qtype;
+        }
+        double th = 0.67, tw = 0.72;
+        if (any_layout) randomise_hw(S, e, th, tw, minor ? JITTER_TARGET_BOUND : -1.0, th, tw);
+        inst_goal(S, e, B, -0.72, -0.22, th, tw, qcol); // entity 1
+        for (int i = 0; i < n_out; i++) // role 1: same colour and shape as the query (target set), 2: distractor
+            inst_block(S, L, e, B, types[i], cols[i], (cols[i] == qcol && types[i] == qtype) ? 1 : 2,
+                       count ? 0.0 : FD_OUT_POSES[i][0], count ? 0.0 : FD_OUT_POSES[i][1],
+                       count ? 0.0 : FD_OUT_POSES[i][2], star_groups);
+        inst_block(S, L, e, B, qtype, qcol, 1, -0.33, -0.49, -0.51, star_groups);
+        const int query = S.nents[e] - 1;
+        inst_robot(S, L, e, B, -0.57, 0.25, 3.83);
+        if (any_layout) {
+            n = 0;
+            ents[n++] = 1;                 // sensor
+            ents[n++] = S.nents[e] - 1;    // robot
+            for (int i = 0; i < n_out; i++) ents[n++] = 2 + i;
+            for (int i = 0; i < n; i++) { rr[i] = i != 0; rl[i] = minor ? JITTER_ROT_BOUND : -1.0; }
+            S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
+            randomise_all(S, L, e, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl, 1u << query);
+            if (!(S.overflow[e] & 2)) { // the query block last, mostly inside the placed sensor
+                double lim = fmin(th, tw) / 2 - L->robot_radius * 0.6 / 2;
+                lim = lim > 0 ? lim : 0.0;
+                if (minor) lim = fmin(JITTER_POS_BOUND, lim);
+                shift_entity(S, e, query, v2(AT(S.ex, 1), AT(S.ey, 1)), AT(S.ba, AT(S.ebody0, query)));
+                if (randomise_pose(S, L, e, query, true, lim, minor ? JITTER_ROT_BOUND : -1.0, 1u << 1) != 0)
+                    S.overflow[e] |= 2;
+            }
+        }
+    } else if (cfg.task == MG_TASK_FIX_COLOUR) { // fix_colour.py:67-176
+        const bool count = (f & MG_RAND_SHAPE_COUNT) != 0;
+        const int nr = count ? mt_randint(S, e, 2, 3 + 1) : 3;
+        int rcols[3], bcols[3], types[3];
+        double rh[3], rw[3];
+        for (int i = 0; i < 3; i++) {
+            const int k = count ? 0 : i;
+            rcols[i] = FC_REGION_COLOURS[i]; bcols[i] = FC_BLOCK_COLOURS[i]; types[i] = FC_BLOCK_TYPES[i];
+            rh[i] = FC_REGIONS[k][2]; rw[i] = FC_REGIONS[k][3];
+        }
+        if (f & MG_RAND_COLOUR) {
+            for (int i = 0; i < nr; i++) rcols[i] = MG_SHAPE_COLOURS[mt_randint(S, e, 0, 4)];
+            for (int i = 0; i < nr; i++) bcols[i] = rcols[i];
+            const int odd = mt_randint(S, e, 0, nr);
+            int nc = mt_randint(S, e, 0, 4 - 1);
+            if (MG_SHAPE_COLOURS[nc] == bcols[odd]) nc++;
+            bcols[odd] = MG_SHAPE_COLOURS[nc];
+        }
+        if (f & MG_RAND_SHAPE_TYPE) for (int i = 0; i < nr; i++) types[i] = MG_SHAPE_TYPES[mt_randint(S, e, 0, 4)];
+        if (any_layout)
+            for (int i = 0; i < nr; i++)
+                randomise_hw(S, e, rh[i], rw[i], minor ? JITTER_TARGET_BOUND : -1.0, rh[i], rw[i], 0.4, 0.5);
+        for (int i = 0; i < nr; i++) { // regions: entities 1 .. nr
+            const int k = count ? 0 : i;
+            inst_goal(S, e, B, FC_REGIONS[k][0], FC_REGIONS[k][1], rh[i], rw[i], rcols[i]);
+        }
+        for (int i = 0; i < nr; i++) { // blocks: entities nr+1 .. 2nr; role 1: matches its region's colour
+            const int k = count ? 0 : i;
+            inst_block(S, L, e, B, types[i], bcols[i], bcols[i] == rcols[i] ? 1 : 2, FC_BLOCK_POSES[k][0],
+                       FC_BLOCK_POSES[k][1], FC_BLOCK_POSES[k][2], star_groups);
+        }
+        inst_robot(S, L, e, B, 0.368, 0.586, 0.718);
+        if (any_layout) {
+            n = 0;
+            uint32_t blocks = 0u;
+            for (int i = 0; i < nr; i++) { ents[n++] = 1 + i; blocks |= 1u << (1 + nr + i); }
+            ents[n++] = S.nents[e] - 1;
+            for (int i = 0; i < n; i++) { rr[i] = i == nr; rl[i] = minor ? JITTER_ROT_BOUND : -1.0; }
+            S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
+            randomise_all(S, L, e, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl, blocks);
+            if (!(S.overflow[e] & 2)) {
+                for (int i = 0; i < nr; i++) {
+                    const int b = 1 + nr + i;
+                    shift_entity(S, e, b, v2(AT(S.ex, 1 + i), AT(S.ey, 1 + i)), AT(S.ba, AT(S.ebody0, b)));
+                }
+                for (int i = 0; i < nr; i++) {
+                    double lim = fmin(rh[i], rw[i]) / 2 - L->robot_radius * 0.6;
+                    lim = lim > 0 ? lim : 0.0;
+                    if (minor) lim = fmin(JITTER_POS_BOUND, lim);
+                    if (randomise_pose(S, L, e, 1 + nr + i, true, lim, minor ? JITTER_ROT_BOUND : -1.0, 1u << (1 + i)) != 0) {
+                        S.overflow[e] |= 2;
+                        break;
+                    }
+                }
+            }
         }
     } else { // MatchRegions
         int target = MG_COL_GREEN;

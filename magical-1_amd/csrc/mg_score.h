@@ -62,13 +62,43 @@ MG_DEV int longest_line(const double *px, const double *py, int n, double inlier
     return best;
 }
 
+// entities.py:803-863 get_overlapping_ents(com_overlap=True) of goal entity ge over the blocks: bit i set
+// when every shape of block i overlaps the goal with its body's position inside the goal's BB
+MG_DEV uint32_t goal_overlap_blocks(const MGState &S, const mg_library *L, int e, int ge) {
+    ShapeW G;
+    load_goal(AT(S.ex, ge), AT(S.ey, ge), AT(S.ew, ge), AT(S.eh, ge), 0, G);
+    const int nents = S.nents[e];
+    uint32_t in = 0u;
+    for (int i = 0; i < nents; i++) {
+        if (AT(S.ekind, i) != MG_ENT_BLOCK) continue;
+        int s0 = AT(S.eshape0, i), ns = AT(S.enshapes, i);
+        bool any = false, all = true;
+        for (int k = s0; k < s0 + ns; k++) {
+            ShapeW A;
+            load_shape(S, L, e, k, 0, A);
+            bool hit = false;
+            if (bb_intersects(G, A)) {
+                Collision info;
+                collide(G, A, info);
+                if (info.count) {
+                    V2 p = v2(AT(S.bpx, A.body), AT(S.bpy, A.body));
+                    hit = G.bbl <= p.x && G.bbr >= p.x && G.bbb <= p.y && G.bbt >= p.y;
+                }
+            }
+            if (hit) any = true; else all = false;
+        }
+        if (any && all) in |= 1u << i;
+    }
+    return in;
+}
+
 MG_DEV double score_env(const MGState &S, const mg_library *L, int e, int task) {
     int rb = S.robot_body0[e];
     V2 rp = v2(AT(S.bpx, rb), AT(S.bpy, rb));
     if (task == MG_TASK_MOVE_TO_REGION) {
         int ge = S.goal_ent[e];
         ShapeW G;
-        load_goal(S.gpx[e], S.gpy[e], AT(S.ew, ge), AT(S.eh, ge), 0, G);
+        load_goal(AT(S.ex, ge), AT(S.ey, ge), AT(S.ew, ge), AT(S.eh, ge), 0, G);
         return poly_point_query(G, rp) <= 0 ? 1.0 : 0.0;
     }
     if (task == MG_TASK_MOVE_TO_CORNER) {
@@ -137,31 +167,38 @@ MG_DEV double score_env(const MGState &S, const mg_library *L, int e, int task) 
         const int min_len = n - 2 > 2 ? n - 2 : 2, d = line_len - min_len;
         return (double)(d > 0 ? d : 0) / (double)(n - min_len);
     }
+    if (task == MG_TASK_FIND_DUPE) { // find_dupe.py:202-216
+        const uint32_t in = goal_overlap_blocks(S, L, e, S.goal_ent[e]);
+        int n_t = 0, n_d = 0, n_in = 0;
+        for (int i = 0; i < nents; i++) {
+            if (!((in >> i) & 1u)) continue;
+            n_in++;
+            if (AT(S.erole, i) == 1) n_t++; else n_d++;
+        }
+        const double have_two = n_t >= 2 ? 1.0 : 0.0;
+        const double contamination = n_in == 0 ? 0.0 : (double)n_d / n_in;
+        return have_two * (1 - contamination);
+    }
+    if (task == MG_TASK_FIX_COLOUR) { // fix_colour.py:181-192: region r holds exactly block r iff it matches
+        int goals[MG_MAX_ENTS], blocks[MG_MAX_ENTS], ng = 0, nb = 0;
+        for (int i = 0; i < nents; i++) {
+            if (AT(S.ekind, i) == MG_ENT_GOAL) goals[ng++] = i;
+            if (AT(S.ekind, i) == MG_ENT_BLOCK) blocks[nb++] = i;
+        }
+        for (int r = 0; r < ng && r < nb; r++) {
+            const uint32_t in = goal_overlap_blocks(S, L, e, goals[r]);
+            const bool want = AT(S.erole, blocks[r]) == 1;
+            if (want ? in != (1u << blocks[r]) : in != 0u) return 0.0;
+        }
+        return 1.0;
+    }
     // MatchRegions
-    int ge = S.goal_ent[e];
-    ShapeW G;
-    load_goal(S.gpx[e], S.gpy[e], AT(S.ew, ge), AT(S.eh, ge), 0, G);
+    const uint32_t in = goal_overlap_blocks(S, L, e, S.goal_ent[e]);
     int n_t = 0, n_d = 0, n_in = 0, total_t = 0;
     for (int i = 0; i < nents; i++) {
         if (AT(S.ekind, i) != MG_ENT_BLOCK) continue;
         if (AT(S.erole, i) == 1) total_t++;
-        int s0 = AT(S.eshape0, i), ns = AT(S.enshapes, i);
-        bool any = false, all = true;
-        for (int k = s0; k < s0 + ns; k++) {
-            ShapeW A;
-            load_shape(S, L, e, k, 0, A);
-            bool hit = false;
-            if (bb_intersects(G, A)) {
-                Collision info;
-                collide(G, A, info);
-                if (info.count) {
-                    V2 p = v2(AT(S.bpx, A.body), AT(S.bpy, A.body));
-                    hit = G.bbl <= p.x && G.bbr >= p.x && G.bbb <= p.y && G.bbt >= p.y;
-                }
-            }
-            if (hit) any = true; else all = false;
-        }
-        if (any && all) {
+        if ((in >> i) & 1u) {
             n_in++;
             if (AT(S.erole, i) == 1) n_t++; else n_d++;
         }

@@ -140,7 +140,7 @@ static void layout(MGState &S, Carver &c) {
     S.ekind = c.take<int8_t>(E); S.etype = c.take<int8_t>(E); S.ecol = c.take<int8_t>(E); S.erole = c.take<int8_t>(E);
     S.ebody0 = c.take<int8_t>(E); S.eshape0 = c.take<int8_t>(E); S.enshapes = c.take<int8_t>(E);
     S.ex = c.take<double>(E); S.ey = c.take<double>(E); S.eang = c.take<double>(E); S.eh = c.take<double>(E);
-    S.ew = c.take<double>(E); S.nents = c.take<int32_t>(N); S.gpx = c.take<double>(N); S.gpy = c.take<double>(N);
+    S.ew = c.take<double>(E); S.nents = c.take<int32_t>(N);
     S.goal_ent = c.take<int32_t>(N); S.episode_steps = c.take<int32_t>(N);
     S.mt_key = c.take<uint32_t>(624 * N); S.mt_pos = c.take<int32_t>(N);
     size_t FR = (size_t)MG_LORES * MG_LORES * 3;
@@ -159,6 +159,8 @@ static StepCaps step_caps(int task, int flags, int n_envs, const mg_library &lib
     case MG_TASK_CLUSTER_COLOUR:
     case MG_TASK_CLUSTER_SHAPE: nblk = (flags & MG_RAND_SHAPE_COUNT) ? 10 : 8; break;
     case MG_TASK_MAKE_LINE: nblk = 4; break;
+    case MG_TASK_FIND_DUPE: nblk = 7; break;
+    case MG_TASK_FIX_COLOUR: nblk = 3; break;
     default: nblk = (flags & MG_RAND_SHAPE_COUNT) ? 8 : 5; break;
     }
     const int per_blk = star_ok ? lib.block_nshapes[MG_SHAPE_STAR] : 1;
@@ -235,7 +237,7 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     if (cfg->library_size != (int64_t)sizeof(mg_library))
         return set_err(-22, "mg_create: library_size mismatch (expected " + std::to_string(sizeof(mg_library)) + ")");
     if (cfg->num_envs <= 0) return set_err(-22, "mg_create: num_envs must be positive");
-    if (cfg->task < 0 || cfg->task > MG_TASK_MAKE_LINE) return set_err(-22, "mg_create: unknown task");
+    if (cfg->task < 0 || cfg->task > MG_TASK_FIX_COLOUR) return set_err(-22, "mg_create: unknown task");
     if (cfg->preproc != MG_PREPROC_LORES4E && cfg->preproc != MG_PREPROC_LORESSTACK &&
         cfg->preproc != MG_PREPROC_LORES4A && cfg->preproc != MG_PREPROC_LORES3EA && cfg->preproc != MG_PREPROC_NONE)
         return set_err(-95, "mg_create: preprocessor not supported by the GPU path");
@@ -353,6 +355,23 @@ int mg_selftest_sincos(const double *x, double *s_out, double *c_out, int n, voi
     if (!x || !s_out || !c_out || n < 0) return set_err(-22, "mg_selftest_sincos: bad argument");
     if (n == 0) return 0;
     hipLaunchKernelGGL(sincos_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), x, s_out, c_out, n);
+    HIPC(hipGetLastError());
+    return 0;
+}
+
+// pymunk Body.angle / Body.position setters (as geom.pm_shift_bodies applies them): parity tests
+__global__ void set_body_pose_kernel(MGState S, int e, int b, double x, double y, double a) {
+    body_set_angle(S, e, b, a);
+    const double c = AT(S.brc, b), sn = AT(S.brs, b);
+    AT(S.bpx, b) = (c * 0.0 + (-sn) * 0.0) + x; // cpBodySetPosition: p = T(cog = 0) + position
+    AT(S.bpy, b) = (sn * 0.0 + c * 0.0) + y;
+}
+
+int mg_set_body_pose(mg_sim *s, int env, int body, double x, double y, double angle, void *stream) {
+    if (!s || env < 0 || env >= s->S.n_envs || body < 0 || body >= MG_MAX_BODIES)
+        return set_err(-22, "mg_set_body_pose: bad argument");
+    HIPC(hipSetDevice(s->device));
+    hipLaunchKernelGGL(set_body_pose_kernel, dim3(1), dim3(1), 0, as_stream(stream), s->S, env, body, x, y, angle);
     HIPC(hipGetLastError());
     return 0;
 }

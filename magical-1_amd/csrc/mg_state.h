@@ -47,8 +47,8 @@ struct MGState {
     int8_t *ekind, *etype, *ecol, *erole, *ebody0, *eshape0, *enshapes;
     double *ex, *ey, *eang, *eh, *ew;
     int32_t *nents;
-    double *gpx, *gpy;       // goal body position [N] (static sensor)
-    int32_t *goal_ent;       // [N] (-1 none)
+    int32_t *goal_ent;       // [N] last goal entity added (-1 none); goal body positions are the goal
+                             // entities' ex/ey (static sensors, moved only by reset randomisers)
     // ---- episode ----
     int32_t *episode_steps;
     // ---- RNG: numpy legacy MT19937 per env ----

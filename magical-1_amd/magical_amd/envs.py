@@ -160,6 +160,11 @@ class VecMagicalEnv:
                                             ctypes.c_void_p(counts.data_ptr()), self._stream()))
         return out, counts
 
+    def set_body_pose(self, env, body, x, y, angle):
+        """Place body `body` of env `env` (Body.position / Body.angle setters; parity tests)."""
+        native.check(self.lib.mg_set_body_pose(self.handle, int(env), int(body), float(x), float(y), float(angle),
+                                               self._stream()))
+
     def errors(self):
         out = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
         native.check(self.lib.mg_get_errors(self.handle, ctypes.c_void_p(out.data_ptr()), self._stream()))

@@ -11,7 +11,7 @@ LIB_PATH = os.path.join(HERE, "libmagical_sim_prof.so" if os.environ.get("MAGICA
                         else "libmagical_sim.so")
 
 EXPORTS = ["mg_create", "mg_bind_outputs", "mg_reset", "mg_step", "mg_render_full", "mg_get_bodies",
-           "mg_get_errors", "mg_seed", "mg_random_actions", "mg_num_envs", "mg_enable_timing", "mg_read_timing",
+           "mg_set_body_pose", "mg_get_errors", "mg_seed", "mg_random_actions", "mg_num_envs", "mg_enable_timing", "mg_read_timing",
            "mg_selftest_sincos", "mg_destroy", "mg_last_error"]
 
 
@@ -52,6 +52,7 @@ def load():
     lib.mg_render_full.argtypes = [vp, vp, vp]
     lib.mg_get_bodies.argtypes = [vp, vp, vp, vp]
     lib.mg_get_errors.argtypes = [vp, vp, vp]
+    lib.mg_set_body_pose.argtypes = [vp, i32, i32, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
     lib.mg_seed.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
     lib.mg_random_actions.argtypes = [vp, vp, u64, u64, vp]
     lib.mg_num_envs.argtypes = [vp]

@@ -15,7 +15,7 @@ from typing import Optional
 LAYOUT_MINOR, LAYOUT_FULL, COLOUR, SHAPE_TYPE, SHAPE_COUNT, DYNAMICS = 1, 2, 4, 8, 16, 32
 
 TASK_IDS = {"MoveToRegion": 0, "MoveToCorner": 1, "ClusterColour": 2, "ClusterShape": 3, "MatchRegions": 4,
-            "MakeLine": 5}
+            "MakeLine": 5, "FindDupe": 6, "FixColour": 7}
 GPU_TASKS = set(TASK_IDS)
 
 PREPROCESSORS = collections.OrderedDict([

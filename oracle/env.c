@@ -136,12 +136,25 @@ int oenv_get_bodies(const OEnv *e, double *out, int max_bodies) {
 
 int oenv_num_arbiters(const OEnv *e) { return e->space.nactive; }
 
+/* pymunk Body.angle / Body.position setters on body b (as geom.pm_shift_bodies applies them),
+ * shapes reindexed: parity tests move blocks to chosen poses before a step */
+void oenv_set_body_pose(OEnv *e, int b, double x, double y, double a) {
+    ophys_body_set_angle(&e->space, b, a);
+    vec2 p = {x, y};
+    ophys_body_set_position(&e->space, b, p);
+    for (int k = 0; k < e->space.nshapes; k++)
+        if (e->space.shapes[k].body == b) ophys_shape_update(&e->space, k);
+}
+
 int oenv_get_entities(const OEnv *e, int *kinds, int *types, int *colours, double *poses) {
     for (int i = 0; i < e->nents; i++) {
         const OEntity *en = &e->ents[i];
         kinds[i] = en->kind; types[i] = en->type; colours[i] = en->colour;
         double x = 0, y = 0, a = 0;
-        if (en->kind == ENT_GOAL) { x = en->gx; y = en->gy; poses[4 * i + 2] = en->gh; poses[4 * i + 3] = en->gw; }
+        if (en->kind == ENT_GOAL) { /* the sensor body's current position (centre), h, w */
+            x = e->space.shapes[en->shape0].sp.x; y = e->space.shapes[en->shape0].sp.y;
+            poses[4 * i + 2] = en->gh; poses[4 * i + 3] = en->gw;
+        }
         else if (en->nbodies > 0) {
             x = e->space.bodies[en->body0].p.x; y = e->space.bodies[en->body0].p.y; a = e->space.bodies[en->body0].a;
             poses[4 * i + 3] = 0;

@@ -119,6 +119,7 @@ void ophys_step(OSpace *s, double dt);
 int ophys_collide(OSpace *s, int a, int b, OCollision *out, int *swapped);
 /* shape_query semantics (cpSpaceShapeQuery / pymunk Space.shape_query): any hit */
 int ophys_shape_query_any(OSpace *s, int sh);
+int ophys_shape_query_any_ign(OSpace *s, int sh, const uint8_t *ign);
 double ophys_poly_point_query(const OShape *sh, vec2 p);
 
 #endif

@@ -37,13 +37,14 @@ typedef struct { double x, y; } vec2;
 #define O_MAX_ARB 96
 #define O_MAX_VERTS 12
 #define O_MAX_ENTS 16
-#define O_MAX_GEOMS 64
+#define O_MAX_GEOMS 192
 #define O_RES 384
 #define O_LORES 96
 
 /* ---- tasks / variants / preprocessors (benchmarks/__init__.py:269-307,427-1102) */
 enum { TASK_MOVE_TO_REGION = 0, TASK_MOVE_TO_CORNER = 1, TASK_CLUSTER_COLOUR = 2,
-       TASK_CLUSTER_SHAPE = 3, TASK_MATCH_REGIONS = 4, TASK_MAKE_LINE = 5 };
+       TASK_CLUSTER_SHAPE = 3, TASK_MATCH_REGIONS = 4, TASK_MAKE_LINE = 5,
+       TASK_FIND_DUPE = 6, TASK_FIX_COLOUR = 7 };
 enum { RAND_LAYOUT_MINOR = 1, RAND_LAYOUT_FULL = 2, RAND_COLOUR = 4, RAND_SHAPE_TYPE = 8,
        RAND_SHAPE_COUNT = 16, RAND_DYNAMICS = 32 };
 enum { PREPROC_NONE = 0, PREPROC_LORES4E = 1, PREPROC_LORESSTACK = 2, PREPROC_LORES3EA = 3,
@@ -96,6 +97,7 @@ void oenv_render_full(OEnv *e, uint8_t *allo, uint8_t *ego);
 /* per dynamic/kinematic body: px, py, a, vx, vy, w  (returns body count) */
 int oenv_get_bodies(const OEnv *e, double *out, int max_bodies);
 int oenv_num_arbiters(const OEnv *e);
+void oenv_set_body_pose(OEnv *e, int body, double x, double y, double angle);
 /* per-env scene summary for tests: entity kinds/types/colours (returns count) */
 int oenv_get_entities(const OEnv *e, int *kinds, int *types, int *colours, double *poses);
 double oenv_last_score(const OEnv *e);

@@ -1000,11 +1000,13 @@ void ophys_step(OSpace *s, double dt) {
 }
 
 /* ---------------- queries ----------------------------------------------- */
-int ophys_shape_query_any(OSpace *s, int si) {
+/* pymunk Space.shape_query (cpSpaceShapeQuery: every shape, sensors included) minus an ignore set
+ * (geom.py:224-226: collisions - ignore_set); ign[j] != 0 ignores shape j, NULL ignores nothing */
+int ophys_shape_query_any_ign(OSpace *s, int si, const uint8_t *ign) {
     OShape *a = &s->shapes[si];
     ophys_shape_update(s, si);
     for (int j = 0; j < s->nshapes; j++) {
-        if (j == si) continue;
+        if (j == si || (ign && ign[j])) continue;
         OShape *b = &s->shapes[j];
         if (!bb_intersects(a, b)) continue;
         if (filter_reject(a, b)) continue;
@@ -1013,6 +1015,8 @@ int ophys_shape_query_any(OSpace *s, int si) {
     }
     return 0;
 }
+
+int ophys_shape_query_any(OSpace *s, int si) { return ophys_shape_query_any_ign(s, si, NULL); }
 
 static vec2 closest_point_on_segment(vec2 p, vec2 a, vec2 b) {
     vec2 delta = vsub(a, b);

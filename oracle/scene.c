@@ -275,6 +275,10 @@ static int add_static_xf(OEnv *e, double tx, double ty) {
     return i;
 }
 static OGeom *add_geom(OEnv *e, int npts, const vec2 *pts, int outline, const uint8_t *col, const uint8_t *ocol) {
+    if (e->ngeoms >= O_MAX_GEOMS) { /* table overflow: reported by oenv_reset/step, last slot reused */
+        e->space.overflow = 1;
+        e->ngeoms = O_MAX_GEOMS - 1;
+    }
     OGeom *g = &e->geoms[e->ngeoms++];
     memset(g, 0, sizeof(*g));
     g->npts = npts;
@@ -617,7 +621,8 @@ static void set_ent_categories(OEnv *e, const OEntity *en, uint32_t cat) {
 }
 
 /* returns 0 on success, -1 on PlacementError */
-static int randomise_pose(OEnv *e, OEntity *en, int rand_pos, int rand_rot, double pos_limit, double rot_limit) {
+static int randomise_pose(OEnv *e, OEntity *en, int rand_pos, int rand_rot, double pos_limit, double rot_limit,
+                          const uint8_t *ign) {
     int ids[8], n;
     ent_bodies(e, en, ids, &n);
     double orig_angle = body_angle(e, ids[0]);
@@ -648,7 +653,7 @@ static int randomise_pose(OEnv *e, OEntity *en, int rand_pos, int rand_rot, doub
         shift_bodies(e, en, npos, nang);
         int reject = 0;
         for (int i = 0; i < en->nshapes && !reject; i++)
-            if (ophys_shape_query_any(&e->space, en->shape0 + i)) reject = 1;
+            if (ophys_shape_query_any_ign(&e->space, en->shape0 + i, ign)) reject = 1;
         if (!reject) return 0;
     }
     for (int k = 0; k < n; k++) {
@@ -662,8 +667,8 @@ static int randomise_pose(OEnv *e, OEntity *en, int rand_pos, int rand_rot, doub
 }
 
 /* geom.py:281-341 */
-static void randomise_all_poses(OEnv *e, const int *ents, int n, const int *rand_rot, double pos_limit,
-                                const double *rot_limits) {
+static void randomise_all_poses_ign(OEnv *e, const int *ents, int n, const int *rand_rot, double pos_limit,
+                                    const double *rot_limits, const uint8_t *ign) {
     for (int retry = 0; retry < 10; retry++) {
         uint32_t saved[O_MAX_ENTS];
         for (int k = 0; k < n; k++) {
@@ -674,11 +679,21 @@ static void randomise_all_poses(OEnv *e, const int *ents, int n, const int *rand
         for (int k = 0; k < n; k++) {
             OEntity *en = &e->ents[ents[k]];
             set_ent_categories(e, en, saved[k]);
-            if (randomise_pose(e, en, 1, rand_rot[k], pos_limit, rot_limits[k]) != 0) { failed = 1; break; }
+            if (randomise_pose(e, en, 1, rand_rot[k], pos_limit, rot_limits[k], ign) != 0) { failed = 1; break; }
         }
         if (!failed) return;
     }
     e->placement_error = 1;
+}
+
+static void randomise_all_poses(OEnv *e, const int *ents, int n, const int *rand_rot, double pos_limit,
+                                const double *rot_limits) {
+    randomise_all_poses_ign(e, ents, n, rand_rot, pos_limit, rot_limits, NULL);
+}
+
+/* ignore set of an entity's shapes (ignore_shapes=entity.shapes) */
+static void ign_add(uint8_t *ign, const OEntity *en) {
+    for (int i = 0; i < en->nshapes; i++) ign[en->shape0 + i] = 1;
 }
 
 /* geom.py:344-359 */
@@ -896,6 +911,138 @@ static void reset_make_line(OEnv *e) {
     }
 }
 
+/* find_dupe.py:7-37 defaults, :62-199 on_reset */
+static const int FD_OUT_TYPES[6] = {SHAPE_PENTAGON, SHAPE_CIRCLE, SHAPE_CIRCLE, SHAPE_SQUARE, SHAPE_STAR, SHAPE_PENTAGON};
+static const int FD_OUT_COLOURS[6] = {COL_GREEN, COL_RED, COL_RED, COL_YELLOW, COL_BLUE, COL_YELLOW};
+static const double FD_OUT_POSES[6][3] = {{-0.066751, 0.7552, -2.9266}, {-0.05195, 0.31468, 1.5418},
+                                          {0.57528, -0.46865, -2.2141},  {0.40594, -0.74977, 0.24582},
+                                          {0.45254, 0.3681, -1.0834},    {0.76849, -0.10652, 0.10028}};
+
+static void reset_find_dupe(OEnv *e) {
+    int f = e->flags;
+    const int layout = (f & (RAND_LAYOUT_MINOR | RAND_LAYOUT_FULL)) != 0, minor = (f & RAND_LAYOUT_MINOR) != 0;
+    int qcol = COL_YELLOW, qtype = SHAPE_PENTAGON;
+    int cols[8], types[8];
+    memcpy(cols, FD_OUT_COLOURS, sizeof(FD_OUT_COLOURS));
+    memcpy(types, FD_OUT_TYPES, sizeof(FD_OUT_TYPES));
+    int n_out = 6;
+    if (f & RAND_SHAPE_COUNT) n_out = (int)o_mt_randint(&e->rng, 1, 5 + 1) + 1;
+    int nd = n_out - 1;
+    if (f & RAND_COLOUR) {
+        qcol = SHAPE_COLOURS[o_mt_randint(&e->rng, 0, 4)];
+        for (int i = 0; i < nd; i++) cols[i] = SHAPE_COLOURS[o_mt_randint(&e->rng, 0, 4)];
+        cols[nd] = qcol;
+    }
+    if (f & RAND_SHAPE_TYPE) {
+        qtype = SHAPE_TYPES[o_mt_randint(&e->rng, 0, 4)];
+        for (int i = 0; i < nd; i++) types[i] = SHAPE_TYPES[o_mt_randint(&e->rng, 0, 4)];
+        types[nd] = qtype;
+    }
+    double tx = -0.72, ty = -0.22, th = 0.67, tw = 0.72;
+    if (layout) randomise_hw(e, 0.5, 0.8, th, tw, minor ? JITTER_TARGET_BOUND : -1, &th, &tw);
+    add_goal(e, tx, ty, th, tw, qcol);
+    int sensor = e->nents - 1;
+    int first = e->nents;
+    for (int i = 0; i < n_out; i++) {
+        const int cnt = (f & RAND_SHAPE_COUNT) != 0; /* [((0, 0), 0)] * n_out */
+        double x = cnt ? 0 : FD_OUT_POSES[i][0], y = cnt ? 0 : FD_OUT_POSES[i][1], a = cnt ? 0 : FD_OUT_POSES[i][2];
+        /* role 1: in the target set (same colour and shape as the query), 2: distractor */
+        add_block(e, types[i], cols[i], v2(x, y), a, (cols[i] == qcol && types[i] == qtype) ? 1 : 2);
+    }
+    add_block(e, qtype, qcol, v2(-0.33, -0.49), -0.51, 1); /* the query block */
+    int query = e->nents - 1;
+    add_robot(e, v2(-0.57, 0.25), 3.83);
+    if (layout) {
+        int ents[16], rr[16]; double rl[16]; int n = 0;
+        ents[n++] = sensor; ents[n++] = e->robot;
+        for (int i = 0; i < n_out; i++) ents[n++] = first + i;
+        for (int i = 0; i < n; i++) { rr[i] = i != 0; rl[i] = minor ? JITTER_ROT_BOUND : -1; }
+        uint8_t ign[O_MAX_SHAPES] = {0};
+        ign_add(ign, &e->ents[query]);
+        randomise_all_poses_ign(e, ents, n, rr, minor ? JITTER_POS_BOUND : -1, rl, ign);
+        if (e->placement_error) return;
+        /* the query block last, mostly inside the (placed) sensor region */
+        double lim = fmin(th, tw) / 2 - shape_rad() / 2;
+        lim = lim > 0 ? lim : 0;
+        if (minor) lim = fmin(JITTER_POS_BOUND, lim);
+        OEntity *q = &e->ents[query];
+        shift_bodies(e, q, e->space.shapes[e->ents[sensor].shape0].sp, e->space.bodies[q->body0].a);
+        uint8_t ign2[O_MAX_SHAPES] = {0};
+        ign_add(ign2, &e->ents[sensor]);
+        if (randomise_pose(e, q, 1, 1, lim, minor ? JITTER_ROT_BOUND : -1, ign2) != 0) e->placement_error = 1;
+    }
+}
+
+/* fix_colour.py:12-41 defaults, :67-176 on_reset */
+static const int FC_BLOCK_COLOURS[3] = {COL_GREEN, COL_GREEN, COL_BLUE};
+static const int FC_BLOCK_TYPES[3] = {SHAPE_PENTAGON, SHAPE_SQUARE, SHAPE_PENTAGON};
+static const double FC_BLOCK_POSES[3][3] = {{0.289, 0.030, 0.307}, {0.133, -0.561, 1.699}, {-0.336, 0.000, -1.529}};
+static const double FC_REGIONS[3][4] = {{-0.032, 0.348, 0.427, 0.468}, {0.019, -0.391, 0.460, 0.458},
+                                        {-0.681, 0.196, 0.498, 0.418}};
+static const int FC_REGION_COLOURS[3] = {COL_GREEN, COL_GREEN, COL_RED};
+
+static void reset_fix_colour(OEnv *e) {
+    int f = e->flags;
+    const int layout = (f & (RAND_LAYOUT_MINOR | RAND_LAYOUT_FULL)) != 0, minor = (f & RAND_LAYOUT_MINOR) != 0;
+    int n = 3;
+    double poses[3][3], regions[3][4];
+    memcpy(poses, FC_BLOCK_POSES, sizeof(poses));
+    memcpy(regions, FC_REGIONS, sizeof(regions));
+    if (f & RAND_SHAPE_COUNT) {
+        n = (int)o_mt_randint(&e->rng, 2, 3 + 1);
+        for (int i = 0; i < n; i++) { memcpy(poses[i], FC_BLOCK_POSES[0], sizeof(poses[i])); memcpy(regions[i], FC_REGIONS[0], sizeof(regions[i])); }
+    }
+    int rcols[3], bcols[3], types[3];
+    memcpy(rcols, FC_REGION_COLOURS, sizeof(rcols));
+    memcpy(bcols, FC_BLOCK_COLOURS, sizeof(bcols));
+    memcpy(types, FC_BLOCK_TYPES, sizeof(types));
+    if (f & RAND_COLOUR) {
+        for (int i = 0; i < n; i++) rcols[i] = SHAPE_COLOURS[o_mt_randint(&e->rng, 0, 4)];
+        for (int i = 0; i < n; i++) bcols[i] = rcols[i];
+        int odd = (int)o_mt_randint(&e->rng, 0, n);
+        int nc = (int)o_mt_randint(&e->rng, 0, 4 - 1);
+        if (SHAPE_COLOURS[nc] == bcols[odd]) nc++;
+        bcols[odd] = SHAPE_COLOURS[nc];
+    }
+    if (f & RAND_SHAPE_TYPE) for (int i = 0; i < n; i++) types[i] = SHAPE_TYPES[o_mt_randint(&e->rng, 0, 4)];
+    if (layout)
+        for (int i = 0; i < n; i++)
+            randomise_hw(e, 0.4, 0.5, regions[i][2], regions[i][3], minor ? JITTER_TARGET_BOUND : -1, &regions[i][2],
+                         &regions[i][3]);
+    int first_sensor = e->nents;
+    for (int i = 0; i < n; i++) add_goal(e, regions[i][0], regions[i][1], regions[i][2], regions[i][3], rcols[i]);
+    int first_block = e->nents;
+    /* role 1: the block matches its region's colour (must stay), 2: the odd one out (must leave) */
+    for (int i = 0; i < n; i++)
+        add_block(e, types[i], bcols[i], v2(poses[i][0], poses[i][1]), poses[i][2], bcols[i] == rcols[i] ? 1 : 2);
+    add_robot(e, v2(0.368, 0.586), 0.718);
+    if (layout) {
+        int ents[8], rr[8]; double rl[8]; int m = 0;
+        for (int i = 0; i < n; i++) ents[m++] = first_sensor + i;
+        ents[m++] = e->robot;
+        for (int i = 0; i < m; i++) { rr[i] = i == n; rl[i] = minor ? JITTER_ROT_BOUND : -1; }
+        uint8_t ign[O_MAX_SHAPES] = {0};
+        for (int i = 0; i < n; i++) ign_add(ign, &e->ents[first_block + i]);
+        randomise_all_poses_ign(e, ents, m, rr, minor ? JITTER_POS_BOUND : -1, rl, ign);
+        if (e->placement_error) return;
+        for (int i = 0; i < n; i++) {
+            OEntity *b = &e->ents[first_block + i];
+            shift_bodies(e, b, e->space.shapes[e->ents[first_sensor + i].shape0].sp, e->space.bodies[b->body0].a);
+        }
+        for (int i = 0; i < n; i++) {
+            double lim = fmin(regions[i][2], regions[i][3]) / 2 - shape_rad();
+            lim = lim > 0 ? lim : 0;
+            if (minor) lim = fmin(JITTER_POS_BOUND, lim);
+            uint8_t ign2[O_MAX_SHAPES] = {0};
+            ign_add(ign2, &e->ents[first_sensor + i]);
+            if (randomise_pose(e, &e->ents[first_block + i], 1, 1, lim, minor ? JITTER_ROT_BOUND : -1, ign2) != 0) {
+                e->placement_error = 1;
+                return;
+            }
+        }
+    }
+}
+
 void oscene_reset(OEnv *e) {
     e->episode_steps = 0;
     e->nents = 0; e->ngeoms = 0; e->nxf = 0; e->robot = -1; e->goal = -1; e->star_groups = 0;
@@ -914,6 +1061,8 @@ void oscene_reset(OEnv *e) {
     case TASK_CLUSTER_SHAPE: reset_cluster(e, 1); break;
     case TASK_MATCH_REGIONS: reset_match_regions(e); break;
     case TASK_MAKE_LINE: reset_make_line(e); break;
+    case TASK_FIND_DUPE: reset_find_dupe(e); break;
+    case TASK_FIX_COLOUR: reset_fix_colour(e); break;
     }
     /* Robot.__init__ control state (entities.py:219-228, 287) */
     e->rel_turn = 0.0;
@@ -1055,10 +1204,12 @@ static double score_cluster(OEnv *e, int by_type) {
     return (v > 0 ? v : 0) / (1 - 0.75);
 }
 
-static double score_match_regions(OEnv *e) {
+/* entities.py:803-863 get_overlapping_ents(com_overlap=True) of goal entity gi over the block
+ * entities: in[i] = 1 if every shape of block i overlaps the goal and has its body's position
+ * inside the goal's BB */
+static void goal_overlap_blocks(OEnv *e, int gi, int *in) {
     OSpace *s = &e->space;
-    OEntity *g = &e->ents[e->goal];
-    int gsi = g->shape0;
+    int gsi = e->ents[gi].shape0;
     ophys_shape_update(s, gsi);
     const OShape *gs = &s->shapes[gsi];
     int overlap[O_MAX_SHAPES] = {0};
@@ -1075,16 +1226,27 @@ static double score_match_regions(OEnv *e) {
             if (gs->bb_l <= p.x && gs->bb_r >= p.x && gs->bb_b <= p.y && gs->bb_t >= p.y) overlap[j] = 1;
         }
     }
+    for (int i = 0; i < e->nents; i++) {
+        OEntity *en = &e->ents[i];
+        in[i] = 0;
+        if (en->kind != ENT_BLOCK) continue;
+        int any = 0, all = 1;
+        for (int k = 0; k < en->nshapes; k++) {
+            if (overlap[en->shape0 + k]) any = 1; else all = 0;
+        }
+        in[i] = any && all;
+    }
+}
+
+static double score_match_regions(OEnv *e) {
+    int in[O_MAX_ENTS];
+    goal_overlap_blocks(e, e->goal, in);
     int n_t = 0, n_d = 0, n_in = 0, total_t = 0;
     for (int i = 0; i < e->nents; i++) {
         OEntity *en = &e->ents[i];
         if (en->kind != ENT_BLOCK) continue;
         if (en->role == 1) total_t++;
-        int any = 0, all = 1;
-        for (int k = 0; k < en->nshapes; k++) {
-            if (overlap[en->shape0 + k]) any = 1; else all = 0;
-        }
-        if (any && all) {
+        if (in[i]) {
             n_in++;
             if (en->role == 1) n_t++;
             else n_d++;
@@ -1093,6 +1255,40 @@ static double score_match_regions(OEnv *e) {
     double frac = (double)n_t / total_t;
     double contamination = n_in == 0 ? 0.0 : (double)n_d / n_in;
     return frac * (1 - contamination);
+}
+
+/* find_dupe.py:202-216 */
+static double score_find_dupe(OEnv *e) {
+    int in[O_MAX_ENTS];
+    goal_overlap_blocks(e, e->goal, in);
+    int n_t = 0, n_d = 0, n_in = 0;
+    for (int i = 0; i < e->nents; i++) {
+        if (!in[i]) continue;
+        n_in++;
+        if (e->ents[i].role == 1) n_t++; else n_d++;
+    }
+    double have_two = n_t >= 2 ? 1.0 : 0.0;
+    double contamination = n_in == 0 ? 0.0 : (double)n_d / n_in;
+    return have_two * (1 - contamination);
+}
+
+/* fix_colour.py:181-192: region i (i-th goal) must hold exactly block i if that block matches its
+ * colour (role 1), and nothing otherwise */
+static double score_fix_colour(OEnv *e) {
+    int goals[8], blocks[8], ng = 0, nb = 0;
+    for (int i = 0; i < e->nents; i++) {
+        if (e->ents[i].kind == ENT_GOAL) goals[ng++] = i;
+        if (e->ents[i].kind == ENT_BLOCK) blocks[nb++] = i;
+    }
+    for (int r = 0; r < ng; r++) {
+        int in[O_MAX_ENTS];
+        goal_overlap_blocks(e, goals[r], in);
+        int cnt = 0;
+        for (int i = 0; i < e->nents; i++) cnt += in[i];
+        int want = e->ents[blocks[r]].role == 1;
+        if (want ? (cnt != 1 || !in[blocks[r]]) : cnt != 0) return 0.0;
+    }
+    return 1.0;
 }
 
 /* make_line.py:33-74 longest_line, in this image's numpy arithmetic: np.linalg.norm of one
@@ -1153,6 +1349,8 @@ double oscene_score(OEnv *e) {
     case TASK_CLUSTER_SHAPE: return score_cluster(e, 1);
     case TASK_MATCH_REGIONS: return score_match_regions(e);
     case TASK_MAKE_LINE: return score_make_line(e);
+    case TASK_FIND_DUPE: return score_find_dupe(e);
+    case TASK_FIX_COLOUR: return score_fix_colour(e);
     }
     return 0.0;
 }

@@ -25,6 +25,12 @@ TASK_CONFIGS = [
     ("MakeLine-Demo-LoRes4E-v0", 3, 185),
     ("MakeLine-TestAll-LoRes4E-v0", 4, 185),
     ("MakeLine-TestCountPlus-LoResStack-v0", 3, 40),
+    ("FindDupe-Demo-LoRes4E-v0", 3, 105),
+    ("FindDupe-TestAll-LoRes4E-v0", 4, 105),
+    ("FindDupe-TestJitter-LoResStack-v0", 3, 30),
+    ("FixColour-Demo-LoRes4E-v0", 3, 65),
+    ("FixColour-TestAll-LoRes4E-v0", 4, 65),
+    ("FixColour-TestJitter-LoRes3EA-v0", 3, 30),
 ]
 # the other observation preprocessors (benchmarks/__init__.py:51-190): same rollout check
 PREPROC_CONFIGS = [
@@ -144,6 +150,8 @@ def test_step_kernel_forms(name, n, steps, env, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["MakeLine-TestLayout-v0", "MakeLine-TestCountPlus-v0", "MatchRegions-TestLayout-v0",
+                                  "FindDupe-TestLayout-v0", "FindDupe-TestAll-v0", "FixColour-TestLayout-v0",
+                                  "FixColour-TestAll-v0",
                                   "ClusterColour-TestLayout-v0", "ClusterShape-TestLayout-v0",
                                   "MoveToRegion-TestLayout-v0", "MoveToCorner-TestAll-v0"])
 def test_scores_on_random_layouts(name):
@@ -175,6 +183,95 @@ def test_scores_on_random_layouts(name):
     assert int(np.abs(errs & ~2).sum()) == 0
     vec.close()
     print(name, "non-zero scores:", int((ref > 0).sum()), "of", n)
+
+
+def _placements(name, kinds, cols, roles_in_goal, poses, rs):
+    """Block poses that make the scorers' outcomes vary: blocks dropped into / pulled out of goal
+    regions, laid along a line (MakeLine) or gathered by colour (ClusterColour)."""
+    goals = [i for i, k in enumerate(kinds) if k == 1]
+    blocks = [i for i, k in enumerate(kinds) if k == 3]
+    out = {}
+    if name.startswith("MakeLine"):
+        o, d = rs.uniform(-0.5, 0.5, 2), rs.uniform(-1, 1, 2)
+        d /= np.linalg.norm(d)
+        for j, b in enumerate(blocks):
+            if rs.rand() < 0.85:
+                t = (j - 1.5) * rs.uniform(0.3, 0.45)
+                out[b] = (*(o + t * d + rs.uniform(-0.12, 0.12, 2)), rs.uniform(-3, 3))
+        return out
+    if name.startswith("Cluster"):
+        centre = {c: rs.uniform(-0.6, 0.6, 2) for c in set(cols)}
+        for b in blocks:
+            if rs.rand() < 0.9:
+                out[b] = (*(centre[cols[b]] + rs.uniform(-0.15, 0.15, 2)), rs.uniform(-3, 3))
+        return out
+    for j, b in enumerate(blocks):
+        r = rs.rand()
+        if name.startswith("FixColour"):
+            g = goals[j] if j < len(goals) else goals[0]
+            if roles_in_goal[b] == 2 and r < 0.7:  # the odd block out
+                out[b] = (rs.uniform(-0.9, 0.9), rs.uniform(-0.9, 0.9), rs.uniform(-3, 3))
+            elif r < 0.2:
+                out[b] = (rs.uniform(-0.9, 0.9), rs.uniform(-0.9, 0.9), rs.uniform(-3, 3))
+            else:
+                continue
+            continue
+        g = goals[rs.randint(len(goals))]
+        want_in = r < (0.7 if roles_in_goal[b] == 1 else 0.15)
+        if want_in:
+            gx, gy, gh, gw = poses[g]
+            out[b] = (gx + rs.uniform(-0.35, 0.35) * gw, gy + rs.uniform(-0.35, 0.35) * gh, rs.uniform(-3, 3))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["FindDupe-Demo-v0", "FindDupe-TestAll-v0", "FixColour-Demo-v0", "FixColour-TestAll-v0",
+                                  "MatchRegions-TestAll-v0", "MakeLine-TestAll-v0", "ClusterColour-TestAll-v0",
+                                  "ClusterShape-TestAll-v0"])
+def test_scores_with_placed_blocks(name):
+    """Blocks are moved (Body.position / angle setters, both sides) into scoring configurations, then
+    one step ends the episode: GPU eval_score == oracle on layouts with every score outcome."""
+    spec = registry.lookup(name)
+    n = 192
+    seeds = [7000 + i for i in range(n)]
+    vec = magical_amd.make_vec(name, n, seeds=seeds, max_episode_steps=1, auto_reset=False)
+    vec.reset()
+    acts = np.random.RandomState(4).randint(0, 18, n)
+    ref = np.zeros(n)
+    skip = np.zeros(n, dtype=bool)
+    for i in range(n):
+        o = po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, 1, seed=seeds[i])
+        try:
+            o.reset()
+        except po.PlacementError:
+            skip[i] = True
+            continue
+        kinds, types, cols, poses = o.entities()
+        body0, nb = {}, 0
+        for k, kind in enumerate(kinds):  # bodies in entity add order: blocks 1, robot 6, others 0
+            body0[k] = nb
+            nb += 1 if kind == 3 else 6 if kind == 2 else 0
+        roles = {}
+        goal = [k for k, kind in enumerate(kinds) if kind == 1]
+        for k, kind in enumerate(kinds):  # role proxy from colours: same colour as (its) goal
+            if kind == 3:
+                roles[k] = 1 if goal and cols[k] == cols[goal[0]] else 2
+        if name.startswith("FixColour"):
+            blocks = [k for k, kind in enumerate(kinds) if kind == 3]
+            roles = {b: (1 if cols[b] == cols[goal[j]] else 2) for j, b in enumerate(blocks)}
+        for b, (x, y, a) in _placements(name, kinds, cols, roles, poses, np.random.RandomState(i)).items():
+            o.set_body_pose(body0[b], x, y, a)
+            vec.set_body_pose(i, body0[b], x, y, a)
+        ref[i] = o.step(int(acts[i]))[3]
+    _, rew, done, info = vec.step(torch.as_tensor(acts, dtype=torch.uint8))
+    got = info["eval_score"].cpu().numpy()
+    errs = vec.errors().cpu().numpy()
+    assert np.array_equal((errs & 2) != 0, skip)
+    assert np.array_equal(got[~skip], ref[~skip]), np.nonzero(got[~skip] != ref[~skip])
+    vals, counts = np.unique(ref[~skip], return_counts=True)
+    print(name, dict(zip(vals.tolist(), counts.tolist())))
+    assert len(vals) >= 2, "placements produced a single score outcome"
+    vec.close()
 
 
 @pytest.mark.gpu
