@@ -32,8 +32,9 @@ extern "C" {
 typedef struct mg_sim mg_sim;
 
 typedef struct {
-    int32_t task;              /* 0 MoveToRegion 1 MoveToCorner 2 ClusterColour 3 ClusterShape 4 MatchRegions 5 MakeLine 6 FindDupe 7 FixColour */
-    int32_t rand_flags;        /* bit 0 layout minor, 1 layout full, 2 colour, 3 shape type, 4 count, 5 dynamics */
+    int32_t task;              /* 0 MoveToRegion 1 MoveToCorner 2 ClusterColour 3 ClusterShape 4 MatchRegions 5 MakeLine 6 FindDupe 7 FixColour 8 PickAndPlace */
+    int32_t rand_flags;        /* bit 0 layout minor, 1 layout full, 2 colour, 3 shape type, 4 count, 5 dynamics,
+                                  6 debug_reward (dense shaped reward: move_to_corner.py:85-100, pick_and_place.py:108-124) */
     int32_t preproc;           /* 0 none, 1 LoRes4E, 2 LoResStack, 4 LoRes4A */
     int32_t num_envs;
     int32_t device;            /* HIP device ordinal */
@@ -53,6 +54,8 @@ typedef struct {
     float *reward;       /* f32[N] (eval_score at done, else 0) */
     uint8_t *done;       /* u8[N] */
     double *eval_score;  /* f64[N] (info['eval_score']) */
+    double *target;      /* PickAndPlace: f64[N,4] = (target_type, target_colour, target_position x, y)
+                            (pick_and_place.py:87-107 observation extras), written at reset; NULL otherwise */
 } mg_buffers;
 
 /* replaces gym.make(name) for N instances (benchmarks/__init__.py:232-266) */

@@ -27,9 +27,10 @@
 // tasks / rand flags / preprocessors (mirror benchmarks/__init__.py:269-307, 427-1102)
 enum { MG_TASK_MOVE_TO_REGION = 0, MG_TASK_MOVE_TO_CORNER = 1, MG_TASK_CLUSTER_COLOUR = 2,
        MG_TASK_CLUSTER_SHAPE = 3, MG_TASK_MATCH_REGIONS = 4, MG_TASK_MAKE_LINE = 5,
-       MG_TASK_FIND_DUPE = 6, MG_TASK_FIX_COLOUR = 7 };
+       MG_TASK_FIND_DUPE = 6, MG_TASK_FIX_COLOUR = 7, MG_TASK_PICK_AND_PLACE = 8 };
 enum { MG_RAND_LAYOUT_MINOR = 1, MG_RAND_LAYOUT_FULL = 2, MG_RAND_COLOUR = 4, MG_RAND_SHAPE_TYPE = 8,
-       MG_RAND_SHAPE_COUNT = 16, MG_RAND_DYNAMICS = 32 };
+       MG_RAND_SHAPE_COUNT = 16, MG_RAND_DYNAMICS = 32,
+       MG_DEBUG_REWARD = 64 /* debug_reward=True (move_to_corner.py:85-100, pick_and_place.py:108-124) */ };
 enum { MG_PREPROC_NONE = 0, MG_PREPROC_LORES4E = 1, MG_PREPROC_LORESSTACK = 2, MG_PREPROC_LORES3EA = 3,
        MG_PREPROC_LORES4A = 4, MG_PREPROC_LORESCHW4E = 5 };
 

@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
     S.episode_steps[e] = steps;
     bool d = max_steps > 0 && steps >= max_steps;
     double sc = d ? score_env(S, L, e, cfg.task) : 0.0;
-    if (reward) reward[e] = (float)sc;
+    if (reward) reward[e] = (float)((cfg.flags & MG_DEBUG_REWARD) ? debug_reward(S, L, e, cfg.task) : sc);
     if (done) done[e] = d ? 1 : 0;
     if (eval_score) eval_score[e] = sc;
     // VecEnv auto-reset (next obs = first frame of the new episode) runs as reset_kernel on this mask

@@ -572,6 +572,37 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
                 }
             }
         }
+    } else if (cfg.task == MG_TASK_PICK_AND_PLACE) { // pick_and_place.py:30-85
+        inst_robot(S, L, e, B, 0.0, 0.0, 0.55 * 3.141592653589793); // entity 1: added before the shapes
+        int cols[3], types[3];
+        for (int i = 0; i < 3; i++) { // per shape: colour draw, then type draw
+            cols[i] = MG_COL_RED; types[i] = MG_SHAPE_SQUARE;
+            if (f & MG_RAND_COLOUR) cols[i] = MG_SHAPE_COLOURS[mt_randint(S, e, 0, 4)];
+            if (f & MG_RAND_SHAPE_TYPE) types[i] = MG_SHAPE_TYPES[mt_randint(S, e, 0, 4)];
+        }
+        for (int i = 0; i < 3; i++)
+            inst_block(S, L, e, B, types[i], cols[i], 0, 0.1, -0.65, 0.13 * 3.141592653589793, star_groups);
+        int tid = 0, cid = 0;
+        for (int k = 0; k < 4; k++) {
+            if (MG_SHAPE_TYPES[k] == types[0]) tid = k;
+            if (MG_SHAPE_COLOURS[k] == cols[0]) cid = k;
+        }
+        const double tx = mt_double(S, e), ty = mt_double(S, e); // rng.rand(2) * 2 - 1
+        S.tgt_x[e] = tx * 2 - 1; S.tgt_y[e] = ty * 2 - 1;
+        S.tgt_ids[e] = tid; S.tgt_ids[N + e] = cid;
+        int valid[3], nv = 0;
+        for (int i = 0; i < 3; i++) if (types[i] == types[0] && cols[i] == cols[0]) valid[nv++] = 2 + i;
+        S.tgt_ent[e] = valid[mt_randint(S, e, 0, nv)]; // rng.choice(valid_target_shapes)
+        if (any_layout) { // rand_poses: robot and shapes, unrestricted
+            n = 4;
+            for (int i = 0; i < 4; i++) { ents[i] = 1 + i; rr[i] = true; rl[i] = -1.0; }
+            S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
+            randomise_all(S, L, e, ents, n, rr, -1.0, rl);
+        }
+        if (S.target_out) {
+            double *t = S.target_out + 4 * (size_t)e;
+            t[0] = tid; t[1] = cid; t[2] = S.tgt_x[e]; t[3] = S.tgt_y[e];
+        }
     } else { // MatchRegions
         int target = MG_COL_GREEN;
         if (f & MG_RAND_COLOUR) target = MG_SHAPE_COLOURS[mt_randint(S, e, 0, 4)];

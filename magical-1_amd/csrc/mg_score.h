@@ -167,6 +167,16 @@ MG_DEV double score_env(const MGState &S, const mg_library *L, int e, int task) 
         const int min_len = n - 2 > 2 ? n - 2 : 2, d = line_len - min_len;
         return (double)(d > 0 ? d : 0) / (double)(n - min_len);
     }
+    if (task == MG_TASK_PICK_AND_PLACE) { // pick_and_place.py:87-101
+        const int tb = AT(S.ebody0, S.tgt_ent[e]);
+        const double dx = S.tgt_x[e] - AT(S.bpx, tb), dy = S.tgt_y[e] - AT(S.bpy, tb);
+        const double dist = sqrt(__fma_rn(dy, dy, dx * dx)); // np.linalg.norm -> BLAS ddot
+        const double succeed = L->robot_radius * 0.6, furthest = sqrt(2.0);
+        const double drange = furthest - succeed;
+        const double v = furthest - dist;
+        const double sc = (v > 0.0 ? v : 0.0) / drange;
+        return sc < 1.0 ? sc : 1.0;
+    }
     if (task == MG_TASK_FIND_DUPE) { // find_dupe.py:202-216
         const uint32_t in = goal_overlap_blocks(S, L, e, S.goal_ent[e]);
         int n_t = 0, n_d = 0, n_in = 0;
@@ -206,4 +216,31 @@ MG_DEV double score_env(const MGState &S, const mg_library *L, int e, int task) 
     double frac = (double)n_t / total_t;
     double contamination = n_in == 0 ? 0.0 : (double)n_d / n_in;
     return frac * (1 - contamination);
+}
+
+// debug_shaped_reward (debug_reward=True): move_to_corner.py:85-100, pick_and_place.py:114-124
+MG_DEV double debug_reward(const MGState &S, const mg_library *L, int e, int task) {
+    const int rb = S.robot_body0[e];
+    const double rx = AT(S.bpx, rb), ry = AT(S.bpy, rb);
+    if (task == MG_TASK_PICK_AND_PLACE) {
+        const int tb = AT(S.ebody0, S.tgt_ent[e]);
+        const double px = AT(S.bpx, tb), py = AT(S.bpy, tb);
+        const double ax = px - S.tgt_x[e], ay = py - S.tgt_y[e];
+        const double s2t = sqrt(__fma_rn(ay, ay, ax * ax));
+        const double bx = rx - px, by = ry - py;
+        const double r2s = sqrt(__fma_rn(by, by, bx * bx));
+        const double rad = L->robot_radius * 0.6;
+        const double shaping = -s2t / 5 - (r2s > rad ? r2s : rad) / 10;
+        return shaping + score_env(S, L, e, task);
+    }
+    int shape = -1; // MoveToCorner: the block
+    for (int i = 0; i < S.nents[e] && shape < 0; i++) if (AT(S.ekind, i) == MG_ENT_BLOCK) shape = i;
+    const int sb = AT(S.ebody0, shape);
+    const double px = AT(S.bpx, sb), py = AT(S.bpy, sb);
+    const double ax = px - 0.0, ay = py - 1.0;
+    const double s2c = sqrt(__fma_rn(ay, ay, ax * ax));
+    const double bx = rx - px, by = ry - py;
+    const double r2s = sqrt(__fma_rn(by, by, bx * bx));
+    const double shaping = -s2c / 5 - (r2s > 0.2 ? r2s : 0.2) / 20;
+    return shaping + score_env(S, L, e, task);
 }

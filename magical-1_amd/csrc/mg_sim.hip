@@ -142,6 +142,9 @@ static void layout(MGState &S, Carver &c) {
     S.ex = c.take<double>(E); S.ey = c.take<double>(E); S.eang = c.take<double>(E); S.eh = c.take<double>(E);
     S.ew = c.take<double>(E); S.nents = c.take<int32_t>(N);
     S.goal_ent = c.take<int32_t>(N); S.episode_steps = c.take<int32_t>(N);
+    S.tgt_ent = c.take<int32_t>(N); S.tgt_ids = c.take<int32_t>(2 * N);
+    S.tgt_x = c.take<double>(N); S.tgt_y = c.take<double>(N);
+    S.target_out = nullptr;
     S.mt_key = c.take<uint32_t>(624 * N); S.mt_pos = c.take<int32_t>(N);
     size_t FR = (size_t)MG_LORES * MG_LORES * 3;
     S.hist_allo = c.take<uint8_t>(4 * N * FR); S.hist_ego = c.take<uint8_t>(4 * N * FR);
@@ -161,6 +164,7 @@ static StepCaps step_caps(int task, int flags, int n_envs, const mg_library &lib
     case MG_TASK_MAKE_LINE: nblk = 4; break;
     case MG_TASK_FIND_DUPE: nblk = 7; break;
     case MG_TASK_FIX_COLOUR: nblk = 3; break;
+    case MG_TASK_PICK_AND_PLACE: nblk = 3; break;
     default: nblk = (flags & MG_RAND_SHAPE_COUNT) ? 8 : 5; break;
     }
     const int per_blk = star_ok ? lib.block_nshapes[MG_SHAPE_STAR] : 1;
@@ -237,7 +241,7 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     if (cfg->library_size != (int64_t)sizeof(mg_library))
         return set_err(-22, "mg_create: library_size mismatch (expected " + std::to_string(sizeof(mg_library)) + ")");
     if (cfg->num_envs <= 0) return set_err(-22, "mg_create: num_envs must be positive");
-    if (cfg->task < 0 || cfg->task > MG_TASK_FIX_COLOUR) return set_err(-22, "mg_create: unknown task");
+    if (cfg->task < 0 || cfg->task > MG_TASK_PICK_AND_PLACE) return set_err(-22, "mg_create: unknown task");
     if (cfg->preproc != MG_PREPROC_LORES4E && cfg->preproc != MG_PREPROC_LORESSTACK &&
         cfg->preproc != MG_PREPROC_LORES4A && cfg->preproc != MG_PREPROC_LORES3EA && cfg->preproc != MG_PREPROC_NONE)
         return set_err(-95, "mg_create: preprocessor not supported by the GPU path");
@@ -296,7 +300,10 @@ int mg_bind_outputs(mg_sim *s, const mg_buffers *b) {
     const void *ptrs[3] = {b->obs_allo, b->obs_ego, b->obs_past};
     for (const void *p : ptrs)
         if (((uintptr_t)p & 15) != 0) return set_err(-22, "mg_bind_outputs: observation buffers must be 16-byte aligned");
+    if (s->task == MG_TASK_PICK_AND_PLACE && !b->target)
+        return set_err(-22, "mg_bind_outputs: target required for PickAndPlace");
     s->out = *b;
+    s->S.target_out = b->target;
     s->bound = 1;
     return 0;
 }

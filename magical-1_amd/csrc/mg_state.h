@@ -51,6 +51,10 @@ struct MGState {
                              // entities' ex/ey (static sensors, moved only by reset randomisers)
     // ---- episode ----
     int32_t *episode_steps;
+    // PickAndPlace (pick_and_place.py:30-85): target shape entity, (type id, colour id), target position
+    int32_t *tgt_ent, *tgt_ids;  // [N], [2][N]
+    double *tgt_x, *tgt_y;       // [N]
+    double *target_out;          // bound output f64[N][4] (target_type, target_colour, x, y) or null
     // ---- RNG: numpy legacy MT19937 per env ----
     uint32_t *mt_key;        // [624][N]
     int32_t *mt_pos;         // [N]

@@ -18,18 +18,19 @@ __all__ = ["ALL_REGISTERED_ENVS", "AVAILABLE_PREPROCESSORS", "DEMO_ENVS_TO_TEST_
 _REGISTERED = False
 
 
-def make(env_name, device="cuda:0", seed=None):
-    """gym.make(env_name) equivalent: one instance, reference single-env API."""
+def make(env_name, device="cuda:0", seed=None, debug_reward=None):
+    """gym.make(env_name[, debug_reward=...]) equivalent: one instance, reference single-env API."""
     from .envs import MagicalEnv
-    return MagicalEnv(env_name, device=device, seed=seed)
+    return MagicalEnv(env_name, device=device, seed=seed, debug_reward=debug_reward)
 
 
-def make_vec(env_name, num_envs, device="cuda:0", seeds=None, base_seed=0, auto_reset=True, max_episode_steps=None):
+def make_vec(env_name, num_envs, device="cuda:0", seeds=None, base_seed=0, auto_reset=True, max_episode_steps=None,
+             debug_reward=None):
     """num_envs instances of env_name on one GPU (batched, auto-resetting).  max_episode_steps
     overrides the registered episode length (gym.make(..., max_episode_steps=...))."""
     from .envs import VecMagicalEnv
     return VecMagicalEnv(env_name, num_envs, device=device, seeds=seeds, base_seed=base_seed, auto_reset=auto_reset,
-                         max_episode_steps=max_episode_steps)
+                         max_episode_steps=max_episode_steps, debug_reward=debug_reward)
 
 
 def register_envs():

@@ -42,20 +42,38 @@ def _obs_shapes(spec):
     return shapes
 
 
+# PickAndPlace observation extras (pick_and_place.py:23-28), inserted after allo/ego by the base env
+# and therefore before the frame stack's past_obs (benchmarks/__init__.py:124-147)
+TARGET_KEYS = ("target_type", "target_colour", "target_position")
+
+
 def observation_space(spec):
-    return spaces.Dict(collections.OrderedDict(
-        (k, spaces.Box(low=0, high=255, shape=s, dtype=np.uint8)) for k, s in _obs_shapes(spec).items()))
+    items = [(k, spaces.Box(low=0, high=255, shape=s, dtype=np.uint8)) for k, s in _obs_shapes(spec).items()]
+    if spec.task == "PickAndPlace":
+        extra = [("target_type", spaces.Box(low=0, high=4, shape=(1,), dtype=np.float32)),
+                 ("target_colour", spaces.Box(low=0, high=4, shape=(1,), dtype=np.float32)),
+                 ("target_position", spaces.Box(low=-1, high=1, shape=(2,), dtype=np.float32))]
+        items = items[:2] + extra + items[2:]
+    return spaces.Dict(collections.OrderedDict(items))
 
 
 class VecMagicalEnv:
     """Batched MAGICAL env on one MI355X (C ABI: include/magical_sim.h)."""
 
     def __init__(self, env_name, num_envs, device="cuda:0", seeds=None, base_seed=0, auto_reset=True,
-                 max_episode_steps=None):
+                 max_episode_steps=None, debug_reward=None):
         self.spec = registry.lookup(env_name)
         if not self.spec.gpu_supported:
             raise NotImplementedError(f"{env_name}: task not on the GPU hot path yet")
         pp = self.spec.preproc
+        if self.spec.task == "PickAndPlace" and pp == "LoResStack":
+            # EagerDictFrameStack concatenates every observation value along the last axis; the
+            # scalar target_type / target_colour make that raise in the reference as well
+            raise ValueError(f"{env_name}: the reference cannot frame-stack PickAndPlace's scalar observations")
+        flags = self.spec.rand_flags
+        if debug_reward is not None:  # gym.make(name, debug_reward=...)
+            flags = (flags | registry.DEBUG_REWARD) if debug_reward else (flags & ~registry.DEBUG_REWARD)
+        self.debug_reward = bool(flags & registry.DEBUG_REWARD)
         self.num_envs = int(num_envs)
         self.device = torch.device(device)
         self.lib = native.load()
@@ -63,7 +81,7 @@ class VecMagicalEnv:
         gpu_pp = {None: 0, "LoRes4E": 1, "LoResStack": 2, "LoRes3EA": 3, "LoRes4A": 4, "LoResCHW4E": 1, "LoResCHW4A": 1}[pp]
         cfg = native.mg_config()
         cfg.task = self.spec.task_id
-        cfg.rand_flags = self.spec.rand_flags
+        cfg.rand_flags = flags
         cfg.preproc = gpu_pp
         cfg.num_envs = self.num_envs
         cfg.device = self.device.index or 0
@@ -97,10 +115,12 @@ class VecMagicalEnv:
         self.reward = torch.zeros(n, dtype=torch.float32, device=dev)
         self.done = torch.zeros(n, dtype=torch.uint8, device=dev)
         self.eval_score = torch.zeros(n, dtype=torch.float64, device=dev)
+        self.target = torch.zeros((n, 4), dtype=torch.float64, device=dev) if self.spec.task == "PickAndPlace" else None
         buf = native.mg_buffers()
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
         buf.obs_allo, buf.obs_ego, buf.obs_past = ptr(self.obs_allo), ptr(self.obs_ego), ptr(self.obs_past)
         buf.reward, buf.done, buf.eval_score = ptr(self.reward), ptr(self.done), ptr(self.eval_score)
+        buf.target = ptr(self.target)
         native.check(self.lib.mg_bind_outputs(self.handle, ctypes.byref(buf)))
         self.action_space = spaces.Discrete(18)
         self.observation_space = observation_space(self.spec)
@@ -111,12 +131,16 @@ class VecMagicalEnv:
 
     def _obs(self):
         if self.spec.preproc is None:
-            return collections.OrderedDict([("allo", self.full[:, 0]), ("ego", self.full[:, 1])])
-        out = collections.OrderedDict([("allo", self.obs_allo), ("ego", self.obs_ego)])
+            out = collections.OrderedDict([("allo", self.full[:, 0]), ("ego", self.full[:, 1])])
+        else:
+            out = collections.OrderedDict([("allo", self.obs_allo), ("ego", self.obs_ego)])
+            if self._chw:
+                out = collections.OrderedDict((k, v.permute(0, 3, 1, 2)) for k, v in out.items())
+        if self.target is not None:  # as SB3's DummyVecEnv buffers them: float32 per the spaces
+            t = self.target.to(torch.float32)
+            out["target_type"], out["target_colour"], out["target_position"] = t[:, 0:1], t[:, 1:2], t[:, 2:4]
         if self.obs_past is not None:
-            out["past_obs"] = self.obs_past
-        if self._chw:
-            out = collections.OrderedDict((k, v.permute(0, 3, 1, 2)) for k, v in out.items())
+            out["past_obs"] = self.obs_past.permute(0, 3, 1, 2) if self._chw else self.obs_past
         return out
 
     # -- API -----------------------------------------------------------------
@@ -187,9 +211,9 @@ class MagicalEnv:
 
     metadata = {"render.modes": ["rgb_array"]}
 
-    def __init__(self, env_name, device="cuda:0", seed=None):
+    def __init__(self, env_name, device="cuda:0", seed=None, debug_reward=None):
         self.spec = registry.lookup(env_name)
-        self._vec = VecMagicalEnv(env_name, 1, device=device, auto_reset=False)
+        self._vec = VecMagicalEnv(env_name, 1, device=device, auto_reset=False, debug_reward=debug_reward)
         self.max_episode_steps = self.spec.max_episode_steps
         self.action_space = spaces.Discrete(18)
         self.observation_space = observation_space(self.spec)
@@ -210,7 +234,14 @@ class MagicalEnv:
         return FLAGS_TO_ACTION_ID[tuple(flags)]
 
     def _np_obs(self, obs):
-        return collections.OrderedDict((k, v[0].cpu().numpy()) for k, v in obs.items())
+        out = collections.OrderedDict()
+        for k, v in obs.items():
+            if k in TARGET_KEYS:  # pick_and_place.py:103-107: python ints and a float64 array
+                t = self._vec.target[0].cpu().numpy()
+                out[k] = int(t[0]) if k == "target_type" else int(t[1]) if k == "target_colour" else t[2:4].copy()
+            else:
+                out[k] = v[0].cpu().numpy()
+        return out
 
     def reset(self):
         self._episode_steps = 0

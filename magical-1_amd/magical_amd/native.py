@@ -25,7 +25,8 @@ class mg_config(ctypes.Structure):
 
 class mg_buffers(ctypes.Structure):
     _fields_ = [("obs_allo", ctypes.c_void_p), ("obs_ego", ctypes.c_void_p), ("obs_past", ctypes.c_void_p),
-                ("reward", ctypes.c_void_p), ("done", ctypes.c_void_p), ("eval_score", ctypes.c_void_p)]
+                ("reward", ctypes.c_void_p), ("done", ctypes.c_void_p), ("eval_score", ctypes.c_void_p),
+                ("target", ctypes.c_void_p)]
 
 
 class NativeError(RuntimeError):

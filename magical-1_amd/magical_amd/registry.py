@@ -13,9 +13,10 @@ from typing import Optional
 
 # rand flag bits (include/magical_sim.h, mg_common.h)
 LAYOUT_MINOR, LAYOUT_FULL, COLOUR, SHAPE_TYPE, SHAPE_COUNT, DYNAMICS = 1, 2, 4, 8, 16, 32
+DEBUG_REWARD = 64  # debug_reward=True: dense shaped reward (move_to_corner.py:85-100, pick_and_place.py:108-124)
 
 TASK_IDS = {"MoveToRegion": 0, "MoveToCorner": 1, "ClusterColour": 2, "ClusterShape": 3, "MatchRegions": 4,
-            "MakeLine": 5, "FindDupe": 6, "FixColour": 7}
+            "MakeLine": 5, "FindDupe": 6, "FixColour": 7, "PickAndPlace": 8}
 GPU_TASKS = set(TASK_IDS)
 
 PREPROCESSORS = collections.OrderedDict([
@@ -110,7 +111,7 @@ class EnvSpec:
 
     @property
     def gpu_supported(self):
-        return self.task in GPU_TASKS and not self.debug_reward
+        return self.task in GPU_TASKS
 
 
 def _f(**kw):
@@ -121,6 +122,7 @@ def _f(**kw):
     if kw.get("shape"): bits |= SHAPE_TYPE
     if kw.get("count"): bits |= SHAPE_COUNT
     if kw.get("dyn"): bits |= DYNAMICS
+    if kw.get("debug"): bits |= DEBUG_REWARD
     return bits
 
 
@@ -139,8 +141,10 @@ _BASE += [("MoveToCorner", v, 80, fl) for v, fl in [
 _BASE += [("MoveToRegion", v, 40, fl) for v, fl in [
     ("Demo", _f()), ("TestJitter", _f(minor=1)), ("TestColour", _f(colour=1)), ("TestLayout", _f(full=1)),
     ("TestDynamics", _f(dyn=1)), ("TestAll", _f(full=1, colour=1, dyn=1))]]
-_BASE += [("PickAndPlace", "Demo", 80, _f(colour=1, shape=1, minor=1)),
-          ("PickAndPlace", "Test", 80, _f(colour=1, shape=1, minor=1))]
+# benchmarks/__init__.py:441-455: rand_shape_colour, rand_shape_type, rand_poses (unrestricted: layout
+# full); the Demo variant is registered with debug_reward=True
+_BASE += [("PickAndPlace", "Demo", 80, _f(colour=1, shape=1, full=1, debug=1)),
+          ("PickAndPlace", "Test", 80, _f(colour=1, shape=1, full=1))]
 
 ALL_REGISTERED_ENVS = []
 SPECS = collections.OrderedDict()
@@ -151,11 +155,11 @@ def _register_all():
     for task, variant, ep_len, flags in _BASE:
         name = f"{task}-{variant}-v0"
         ALL_REGISTERED_ENVS.append(name)
-        SPECS[name] = EnvSpec(name, task, variant, flags, None, ep_len)
+        SPECS[name] = EnvSpec(name, task, variant, flags, None, ep_len, debug_reward=bool(flags & DEBUG_REWARD))
         for pp in PREPROCESSORS:
             new = update_magical_env_name(name, preproc=pp)
             ALL_REGISTERED_ENVS.append(new)
-            SPECS[new] = EnvSpec(new, task, variant, flags, pp, ep_len)
+            SPECS[new] = EnvSpec(new, task, variant, flags, pp, ep_len, debug_reward=bool(flags & DEBUG_REWARD))
     train_to_test = {}
     for name in ALL_REGISTERED_ENVS:
         p = EnvName(name)
@@ -165,11 +169,11 @@ def _register_all():
     # benchmarks/__init__.py:1074-1100: registered with the UNWRAPPED env (no preprocessing)
     dbg = "MoveToCorner-Demo-DebugReward-v0"
     ALL_REGISTERED_ENVS.append(dbg)
-    SPECS[dbg] = EnvSpec(dbg, "MoveToCorner", "Demo", 0, None, 80, debug_reward=True)
+    SPECS[dbg] = EnvSpec(dbg, "MoveToCorner", "Demo", DEBUG_REWARD, None, 80, debug_reward=True)
     for pp in PREPROCESSORS:
         n = f"MoveToCorner-Demo-DebugReward-{pp}-v0"
         ALL_REGISTERED_ENVS.append(n)
-        SPECS[n] = EnvSpec(n, "MoveToCorner", "Demo", 0, None, 80, debug_reward=True)
+        SPECS[n] = EnvSpec(n, "MoveToCorner", "Demo", DEBUG_REWARD, None, 80, debug_reward=True)
 
 
 _register_all()

@@ -109,7 +109,7 @@ int oenv_step(OEnv *e, int action, uint8_t *obs, double *reward, int *done, doub
     double score = 0.0;
     if (d) score = oscene_score(e);
     e->last_score = score;
-    if (reward) *reward = score;
+    if (reward) *reward = (e->flags & DEBUG_REWARD) ? oscene_debug_reward(e) : score;
     if (done) *done = d;
     if (eval_score) *eval_score = score;
     uint8_t *a = (uint8_t *)malloc((size_t)O_RES * O_RES * 3), *g = (uint8_t *)malloc((size_t)O_RES * O_RES * 3);
@@ -138,6 +138,10 @@ int oenv_num_arbiters(const OEnv *e) { return e->space.nactive; }
 
 /* pymunk Body.angle / Body.position setters on body b (as geom.pm_shift_bodies applies them),
  * shapes reindexed: parity tests move blocks to chosen poses before a step */
+void oenv_get_target(const OEnv *e, double out[4]) {
+    out[0] = e->target_type_id; out[1] = e->target_colour_id; out[2] = e->target_pos.x; out[3] = e->target_pos.y;
+}
+
 void oenv_set_body_pose(OEnv *e, int b, double x, double y, double a) {
     ophys_body_set_angle(&e->space, b, a);
     vec2 p = {x, y};

@@ -44,9 +44,10 @@ typedef struct { double x, y; } vec2;
 /* ---- tasks / variants / preprocessors (benchmarks/__init__.py:269-307,427-1102) */
 enum { TASK_MOVE_TO_REGION = 0, TASK_MOVE_TO_CORNER = 1, TASK_CLUSTER_COLOUR = 2,
        TASK_CLUSTER_SHAPE = 3, TASK_MATCH_REGIONS = 4, TASK_MAKE_LINE = 5,
-       TASK_FIND_DUPE = 6, TASK_FIX_COLOUR = 7 };
+       TASK_FIND_DUPE = 6, TASK_FIX_COLOUR = 7, TASK_PICK_AND_PLACE = 8 };
 enum { RAND_LAYOUT_MINOR = 1, RAND_LAYOUT_FULL = 2, RAND_COLOUR = 4, RAND_SHAPE_TYPE = 8,
-       RAND_SHAPE_COUNT = 16, RAND_DYNAMICS = 32 };
+       RAND_SHAPE_COUNT = 16, RAND_DYNAMICS = 32,
+       DEBUG_REWARD = 64 /* debug_reward=True: dense shaped reward (move_to_corner.py:85-100, pick_and_place.py:108-124) */ };
 enum { PREPROC_NONE = 0, PREPROC_LORES4E = 1, PREPROC_LORESSTACK = 2, PREPROC_LORES3EA = 3,
        PREPROC_LORES4A = 4, PREPROC_LORESCHW4E = 5 };
 
@@ -98,6 +99,8 @@ void oenv_render_full(OEnv *e, uint8_t *allo, uint8_t *ego);
 int oenv_get_bodies(const OEnv *e, double *out, int max_bodies);
 int oenv_num_arbiters(const OEnv *e);
 void oenv_set_body_pose(OEnv *e, int body, double x, double y, double angle);
+/* PickAndPlace observation extras: (target_type, target_colour, target_position x, y) */
+void oenv_get_target(const OEnv *e, double out[4]);
 /* per-env scene summary for tests: entity kinds/types/colours (returns count) */
 int oenv_get_entities(const OEnv *e, int *kinds, int *types, int *colours, double *poses);
 double oenv_last_score(const OEnv *e);

@@ -52,6 +52,9 @@ struct OEnv {
     int episode_steps;
     int placement_error; /* geom.py:335-336: PlacementError after max_retries */
     double last_score;
+    /* PickAndPlace (pick_and_place.py:30-85): target shape entity, ids, position */
+    int target_ent, target_type_id, target_colour_id;
+    vec2 target_pos;
     /* LoRes frame history (newest last) */
     uint8_t hist_allo[4][O_LORES * O_LORES * 3];
     uint8_t hist_ego[4][O_LORES * O_LORES * 3];
@@ -62,6 +65,7 @@ void oscene_reset(OEnv *e);
 void oscene_robot_update(OEnv *e);
 void oscene_set_action(OEnv *e, int action);
 double oscene_score(OEnv *e);
+double oscene_debug_reward(OEnv *e);
 int o_longest_line(const double *px, const double *py, int n, double inlier_dist, double max_sep);
 void oscene_pre_draw(OEnv *e);
 /* raster.c */

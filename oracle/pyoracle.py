@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "libmg_oracle.so")
 
 TASKS = {"MoveToRegion": 0, "MoveToCorner": 1, "ClusterColour": 2, "ClusterShape": 3, "MatchRegions": 4,
-         "MakeLine": 5, "FindDupe": 6, "FixColour": 7}
+         "MakeLine": 5, "FindDupe": 6, "FixColour": 7, "PickAndPlace": 8}
 PREPROCS = {None: 0, "LoRes4E": 1, "LoResStack": 2, "LoRes3EA": 3, "LoRes4A": 4, "LoResCHW4E": 5, "LoResCHW4A": 5}
 
 _lib = None
@@ -52,6 +52,7 @@ def lib():
         L.o_mt_randint.restype = ctypes.c_int64; L.o_mt_randint.argtypes = [vp, ctypes.c_int64, ctypes.c_int64]
         L.o_longest_line.restype = i; L.o_longest_line.argtypes = [vp, vp, i, d, d]
         L.oenv_set_body_pose.argtypes = [vp, i, d, d, d]
+        L.oenv_get_target.argtypes = [vp, vp]
         L.o_mt_interval.restype = ctypes.c_uint64; L.o_mt_interval.argtypes = [vp, ctypes.c_uint64]
         L.o_convex_hull.restype = i; L.o_convex_hull.argtypes = [i, vp, vp, vp, d]
         L.o_moment_for_poly.restype = d
@@ -158,6 +159,12 @@ class OracleEnv:
 
     def set_body_pose(self, body, x, y, angle):
         self.L.oenv_set_body_pose(self.h, int(body), float(x), float(y), float(angle))
+
+    def target(self):
+        """PickAndPlace extras: (target_type, target_colour, target_position x, y)"""
+        out = np.zeros(4)
+        self.L.oenv_get_target(self.h, ptr(out))
+        return out
 
     def phys_vars(self):
         out = np.zeros(5)

@@ -1043,6 +1043,33 @@ static void reset_fix_colour(OEnv *e) {
     }
 }
 
+/* pick_and_place.py:30-85 */
+static void reset_pick_and_place(OEnv *e) {
+    int f = e->flags;
+    add_robot(e, v2(0.0, 0.0), 0.55 * M_PI); /* added first: arena, robot, shapes */
+    int cols[3], types[3], first = e->nents;
+    for (int i = 0; i < 3; i++) { /* per shape: colour draw, then type draw (rng.choice of one element) */
+        cols[i] = COL_RED; types[i] = SHAPE_SQUARE;
+        if (f & RAND_COLOUR) cols[i] = SHAPE_COLOURS[o_mt_randint(&e->rng, 0, 4)];
+        if (f & RAND_SHAPE_TYPE) types[i] = SHAPE_TYPES[o_mt_randint(&e->rng, 0, 4)];
+    }
+    for (int i = 0; i < 3; i++) add_block(e, types[i], cols[i], v2(0.1, -0.65), 0.13 * M_PI, 0);
+    for (int k = 0; k < 4; k++) {
+        if (SHAPE_TYPES[k] == types[0]) e->target_type_id = k;
+        if (SHAPE_COLOURS[k] == cols[0]) e->target_colour_id = k;
+    }
+    double tx = o_mt_double(&e->rng), ty = o_mt_double(&e->rng); /* rng.rand(2) * 2 - 1 */
+    e->target_pos = v2(tx * 2 - 1, ty * 2 - 1);
+    int valid[3], nv = 0;
+    for (int i = 0; i < 3; i++) if (types[i] == types[0] && cols[i] == cols[0]) valid[nv++] = first + i;
+    e->target_ent = valid[o_mt_randint(&e->rng, 0, nv)]; /* rng.choice(valid_target_shapes) */
+    if (f & (RAND_LAYOUT_MINOR | RAND_LAYOUT_FULL)) { /* rand_poses: unrestricted */
+        int ents[4] = {e->robot, first, first + 1, first + 2}, rr[4] = {1, 1, 1, 1};
+        double rl[4] = {-1, -1, -1, -1};
+        randomise_all_poses(e, ents, 4, rr, -1, rl);
+    }
+}
+
 void oscene_reset(OEnv *e) {
     e->episode_steps = 0;
     e->nents = 0; e->ngeoms = 0; e->nxf = 0; e->robot = -1; e->goal = -1; e->star_groups = 0;
@@ -1063,6 +1090,7 @@ void oscene_reset(OEnv *e) {
     case TASK_MAKE_LINE: reset_make_line(e); break;
     case TASK_FIND_DUPE: reset_find_dupe(e); break;
     case TASK_FIX_COLOUR: reset_fix_colour(e); break;
+    case TASK_PICK_AND_PLACE: reset_pick_and_place(e); break;
     }
     /* Robot.__init__ control state (entities.py:219-228, 287) */
     e->rel_turn = 0.0;
@@ -1341,6 +1369,39 @@ static double score_make_line(OEnv *e) {
     return (double)(d > 0 ? d : 0) / (double)(n - min_len);
 }
 
+/* norm of a 2-vector as np.linalg.norm computes it (sqrt of BLAS ddot) */
+static double np_norm2(double x, double y) { return sqrt(fma(y, y, x * x)); }
+
+/* pick_and_place.py:87-101 (every valid shape is scored with self.target_shape: one value) */
+static double score_pick_and_place(OEnv *e) {
+    vec2 p = e->space.bodies[e->ents[e->target_ent].body0].p;
+    double dist = np_norm2(e->target_pos.x - p.x, e->target_pos.y - p.y);
+    double succeed = shape_rad(), furthest = sqrt(2.0);
+    double drange = furthest - succeed;
+    double v = furthest - dist;
+    double score = (v > 0.0 ? v : 0.0) / drange;
+    return score < 1.0 ? score : 1.0;
+}
+
+/* debug_shaped_reward: move_to_corner.py:85-100, pick_and_place.py:114-124 */
+double oscene_debug_reward(OEnv *e) {
+    vec2 r = e->space.bodies[e->ents[e->robot].body0].p;
+    if (e->task == TASK_PICK_AND_PLACE) {
+        vec2 p = e->space.bodies[e->ents[e->target_ent].body0].p;
+        double s2t = np_norm2(p.x - e->target_pos.x, p.y - e->target_pos.y);
+        double r2s = np_norm2(r.x - p.x, r.y - p.y);
+        double shaping = -s2t / 5 - (r2s > shape_rad() ? r2s : shape_rad()) / 10;
+        return shaping + score_pick_and_place(e);
+    }
+    int shape = -1; /* MoveToCorner: the block */
+    for (int i = 0; i < e->nents; i++) if (e->ents[i].kind == ENT_BLOCK) { shape = i; break; }
+    vec2 p = e->space.bodies[e->ents[shape].body0].p;
+    double s2c = np_norm2(p.x - 0.0, p.y - 1.0);
+    double r2s = np_norm2(r.x - p.x, r.y - p.y);
+    double shaping = -s2c / 5 - (r2s > 0.2 ? r2s : 0.2) / 20;
+    return shaping + oscene_score(e);
+}
+
 double oscene_score(OEnv *e) {
     switch (e->task) {
     case TASK_MOVE_TO_REGION: return score_move_to_region(e);
@@ -1351,6 +1412,7 @@ double oscene_score(OEnv *e) {
     case TASK_MAKE_LINE: return score_make_line(e);
     case TASK_FIND_DUPE: return score_find_dupe(e);
     case TASK_FIX_COLOUR: return score_fix_colour(e);
+    case TASK_PICK_AND_PLACE: return score_pick_and_place(e);
     }
     return 0.0;
 }

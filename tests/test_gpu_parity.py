@@ -31,6 +31,11 @@ TASK_CONFIGS = [
     ("FixColour-Demo-LoRes4E-v0", 3, 65),
     ("FixColour-TestAll-LoRes4E-v0", 4, 65),
     ("FixColour-TestJitter-LoRes3EA-v0", 3, 30),
+    # the fork's own training configs: train_rl.py:87-92 (PickAndPlace, debug_reward), train_il.py:216
+    ("PickAndPlace-Demo-LoResCHW4A-v0", 4, 85),
+    ("PickAndPlace-Test-LoRes4A-v0", 3, 85),
+    ("PickAndPlace-Demo-v0", 2, 12),
+    ("MoveToCorner-Demo-DebugReward-v0", 2, 85),
 ]
 # the other observation preprocessors (benchmarks/__init__.py:51-190): same rollout check
 PREPROC_CONFIGS = [
@@ -57,6 +62,15 @@ def oracle_env(spec, seed):
     return po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, spec.max_episode_steps, seed=seed)
 
 
+def with_targets(spec, ref, orc):
+    """PickAndPlace observation extras (pick_and_place.py:103-107) as the vec env delivers them:
+    float32 [1], [1], [2] (the spaces' dtype, as SB3's DummyVecEnv buffers them)."""
+    if spec.task == "PickAndPlace":
+        t = orc.target().astype(np.float32)
+        ref["target_type"], ref["target_colour"], ref["target_position"] = t[0:1], t[1:2], t[2:4]
+    return ref
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,n,steps", CONFIGS + PREPROC_CONFIGS + TASK_CONFIGS)
 def test_rollout_parity(name, n, steps):
@@ -66,7 +80,8 @@ def test_rollout_parity(name, n, steps):
     orc = [oracle_env(spec, s) for s in seeds]
     acts = np.random.RandomState(42).randint(0, 18, (steps, n))
     obs = vec.reset()
-    ref = [oracle_obs_split(spec, o.reset()) for o in orc]
+    ref = [with_targets(spec, oracle_obs_split(spec, o.reset()), o) for o in orc]
+    assert list(obs.keys()) == list(vec.observation_space.spaces.keys())
     for k in obs:
         got = obs[k].cpu().numpy()
         for i in range(n):
@@ -91,7 +106,7 @@ def test_rollout_parity(name, n, steps):
                 diff = np.abs(bodies[i, :len(b)] - b).max()
                 max_pose = max(max_pose, diff)
                 assert diff <= POSE_TOL, f"step {t} env {i} body state diff {diff}"
-            ref = oracle_obs_split(spec, o)
+            ref = with_targets(spec, oracle_obs_split(spec, o), orc[i])
             for k in got_obs:
                 assert np.array_equal(got_obs[k][i], ref[k]), f"step {t} env {i} obs {k}"
     assert int(vec.errors().abs().sum().item()) == 0
@@ -185,7 +200,7 @@ def test_scores_on_random_layouts(name):
     print(name, "non-zero scores:", int((ref > 0).sum()), "of", n)
 
 
-def _placements(name, kinds, cols, roles_in_goal, poses, rs):
+def _placements(name, kinds, cols, roles_in_goal, poses, rs, targets=None):
     """Block poses that make the scorers' outcomes vary: blocks dropped into / pulled out of goal
     regions, laid along a line (MakeLine) or gathered by colour (ClusterColour)."""
     goals = [i for i, k in enumerate(kinds) if k == 1]
@@ -198,6 +213,12 @@ def _placements(name, kinds, cols, roles_in_goal, poses, rs):
             if rs.rand() < 0.85:
                 t = (j - 1.5) * rs.uniform(0.3, 0.45)
                 out[b] = (*(o + t * d + rs.uniform(-0.12, 0.12, 2)), rs.uniform(-3, 3))
+        return out
+    if name.startswith("PickAndPlace"):
+        tx, ty = targets[2], targets[3]
+        for b in blocks:
+            if rs.rand() < 0.7:
+                out[b] = (tx + rs.uniform(-0.3, 0.3), ty + rs.uniform(-0.3, 0.3), rs.uniform(-3, 3))
         return out
     if name.startswith("Cluster"):
         centre = {c: rs.uniform(-0.6, 0.6, 2) for c in set(cols)}
@@ -227,7 +248,7 @@ def _placements(name, kinds, cols, roles_in_goal, poses, rs):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["FindDupe-Demo-v0", "FindDupe-TestAll-v0", "FixColour-Demo-v0", "FixColour-TestAll-v0",
                                   "MatchRegions-TestAll-v0", "MakeLine-TestAll-v0", "ClusterColour-TestAll-v0",
-                                  "ClusterShape-TestAll-v0"])
+                                  "ClusterShape-TestAll-v0", "PickAndPlace-Demo-v0", "PickAndPlace-Test-v0"])
 def test_scores_with_placed_blocks(name):
     """Blocks are moved (Body.position / angle setters, both sides) into scoring configurations, then
     one step ends the episode: GPU eval_score == oracle on layouts with every score outcome."""
@@ -237,7 +258,7 @@ def test_scores_with_placed_blocks(name):
     vec = magical_amd.make_vec(name, n, seeds=seeds, max_episode_steps=1, auto_reset=False)
     vec.reset()
     acts = np.random.RandomState(4).randint(0, 18, n)
-    ref = np.zeros(n)
+    ref, rref = np.zeros(n), np.zeros(n)
     skip = np.zeros(n, dtype=bool)
     for i in range(n):
         o = po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, 1, seed=seeds[i])
@@ -259,17 +280,19 @@ def test_scores_with_placed_blocks(name):
         if name.startswith("FixColour"):
             blocks = [k for k, kind in enumerate(kinds) if kind == 3]
             roles = {b: (1 if cols[b] == cols[goal[j]] else 2) for j, b in enumerate(blocks)}
-        for b, (x, y, a) in _placements(name, kinds, cols, roles, poses, np.random.RandomState(i)).items():
+        tg = o.target() if spec.task == "PickAndPlace" else None
+        for b, (x, y, a) in _placements(name, kinds, cols, roles, poses, np.random.RandomState(i), tg).items():
             o.set_body_pose(body0[b], x, y, a)
             vec.set_body_pose(i, body0[b], x, y, a)
-        ref[i] = o.step(int(acts[i]))[3]
+        _, rref[i], _, ref[i] = o.step(int(acts[i]))
     _, rew, done, info = vec.step(torch.as_tensor(acts, dtype=torch.uint8))
     got = info["eval_score"].cpu().numpy()
+    assert np.array_equal(rew.cpu().numpy()[~skip], rref[~skip].astype(np.float32))
     errs = vec.errors().cpu().numpy()
     assert np.array_equal((errs & 2) != 0, skip)
     assert np.array_equal(got[~skip], ref[~skip]), np.nonzero(got[~skip] != ref[~skip])
-    vals, counts = np.unique(ref[~skip], return_counts=True)
-    print(name, dict(zip(vals.tolist(), counts.tolist())))
+    vals = np.unique(ref[~skip])
+    print(name, f"{len(vals)} distinct scores; zero {int((ref[~skip] == 0).sum())}, one {int((ref[~skip] == 1).sum())}")
     assert len(vals) >= 2, "placements produced a single score outcome"
     vec.close()
 
