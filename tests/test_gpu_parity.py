@@ -458,3 +458,44 @@ def test_every_registered_name():
         vec.close()
         checked += 1
     assert checked == len(registry.ALL_REGISTERED_ENVS) - 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["PickAndPlace-Demo-LoResCHW4A-v0", "MoveToCorner-Demo-LoRes4E-v0"])
+def test_sb3_vec_env(name):
+    """SB3 VecEnv adapter (train_rl.py:87-92 DummyVecEnv + Monitor): auto-reset obs = first frame of the
+    next episode, info['terminal_observation'] = last frame of the finished one, Monitor episode
+    return/length, eval_score in every info; all against oracle episodes."""
+    from magical_amd.sb3 import MagicalVecEnv
+    spec = registry.lookup(name)
+    n, T, L = 3, 13, 5
+    seeds = [21, 22, 23]
+    venv = MagicalVecEnv(name, n, seeds=seeds, max_episode_steps=L)
+    orc = [po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, L, seed=s) for s in seeds]
+    obs = venv.reset()
+    ref = [with_targets(spec, oracle_obs_split(spec, o.reset()), o) for o in orc]
+    ret = np.zeros(n)
+    acts = np.random.RandomState(8).randint(0, 18, (T, n))
+    for t in range(T):
+        for i in range(n):
+            for k in obs:
+                assert np.array_equal(obs[k][i], ref[i][k]), (t, i, k)
+        obs, rew, dones, infos = venv.step(acts[t])
+        assert rew.dtype == np.float32 and dones.dtype == bool and len(infos) == n
+        for i in range(n):
+            o, r, d, s = orc[i].step(int(acts[t, i]))
+            ret[i] += np.float32(r)
+            assert rew[i] == np.float32(r) and dones[i] == d and infos[i]["eval_score"] == s
+            last = with_targets(spec, oracle_obs_split(spec, o), orc[i])
+            if d:
+                term = infos[i]["terminal_observation"]
+                for k in term:
+                    assert np.array_equal(term[k], last[k]), (t, i, k)
+                assert infos[i]["episode"]["l"] == L and infos[i]["TimeLimit.truncated"] is False
+                assert abs(infos[i]["episode"]["r"] - ret[i]) < 1e-5
+                ret[i] = 0.0
+                ref[i] = with_targets(spec, oracle_obs_split(spec, orc[i].reset()), orc[i])
+            else:
+                assert "terminal_observation" not in infos[i]
+                ref[i] = last
+    venv.close()
