@@ -190,6 +190,17 @@ MG_DEV void mg_mat3_mul(const double *a, const double *b, double *out) {
     for (int i = 0; i < 9; i++) out[i] = t[i];
 }
 
+// render.py Transform(translation=(tx,ty), rotation) with unit scale: (T @ R) @ S, from the rotation's
+// (sin, cos)
+MG_DEV void mg_transform_tr_sc(double tx, double ty, double s, double c, double *out) {
+    const double T[9] = {1.0, 0.0, tx, 0.0, 1.0, ty, 0.0, 0.0, 1.0};
+    const double R[9] = {c, -s, 0.0, s, c, 0.0, 0.0, 0.0, 1.0};
+    const double S[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0};
+    double TR[9];
+    mg_mat3_mul(T, R, TR);
+    mg_mat3_mul(TR, S, out);
+}
+
 // render.py Transform(translation=(tx,ty), rotation) with unit scale: (T @ R) @ S
 MG_DEV void mg_transform_tr(double tx, double ty, double rot, double *out) {
     double s, c;

@@ -346,22 +346,37 @@ MG_DEV void rpoly_pt(const MGState &S, const mg_library *L, int e, const mg_rpol
     y = (i == 0 || i == 1) ? rad_h : -rad_h;
 }
 
-// render.py Transform matrices of one entity (pre_draw: entities.py:478-491, 751-754, 865-868)
-MG_DEV void entity_xforms(const MGState &S, int e, int ent, double (*xf)[9]) {
-    int kind = AT(S.ekind, ent);
+// (sin, cos) of body b's angle: the physics' rotation cache (body_set_angle: the same correctly rounded
+// sincos of the same angle) when it is current, else computed
+MG_DEV void body_sincos(const MGState &S, int e, int b, double &s, double &c) {
+    const double a = AT(S.ba, b);
+    if (AT(S.bacache, b) == a) { s = AT(S.brs, b); c = AT(S.brc, b); }
+    else mg_sincos(a, s, c);
+}
+
+// render.py Transform matrix x of one entity (pre_draw: entities.py:478-491, 751-754, 865-868); one
+// thread per (entity, transform)
+MG_DEV void entity_xform(const MGState &S, int e, int ent, int x, double *xf) {
+    const int kind = AT(S.ekind, ent);
+    double s, c;
     if (kind == MG_ENT_ROBOT) {
-        int b = AT(S.ebody0, ent);
-        mg_transform_tr(AT(S.bpx, b), AT(S.bpy, b), AT(S.ba, b), xf[MG_XF_MAIN]);
-        for (int k = 0; k < 2; k++) {
-            int fb = b + 4 + k;
-            mg_transform_tr(AT(S.bpx, fb), AT(S.bpy, fb), AT(S.ba, fb), xf[MG_XF_FINGER_L + k]);
-            mg_transform_tr(0.0, 0.0, AT(S.ba, b + 2 + k) - AT(S.ba, b), xf[MG_XF_PUPIL_L + k]);
+        const int b = AT(S.ebody0, ent);
+        if (x == MG_XF_MAIN) {
+            body_sincos(S, e, b, s, c);
+            mg_transform_tr_sc(AT(S.bpx, b), AT(S.bpy, b), s, c, xf);
+        } else if (x == MG_XF_FINGER_L || x == MG_XF_FINGER_R) {
+            const int fb = b + 4 + (x - MG_XF_FINGER_L);
+            body_sincos(S, e, fb, s, c);
+            mg_transform_tr_sc(AT(S.bpx, fb), AT(S.bpy, fb), s, c, xf);
+        } else if (x == MG_XF_PUPIL_L || x == MG_XF_PUPIL_R) {
+            mg_transform_tr(0.0, 0.0, AT(S.ba, b + 2 + (x - MG_XF_PUPIL_L)) - AT(S.ba, b), xf);
         }
-    } else if (kind == MG_ENT_BLOCK) {
-        int b = AT(S.ebody0, ent);
-        mg_transform_tr(AT(S.bpx, b), AT(S.bpy, b), AT(S.ba, b), xf[MG_XF_MAIN]);
-    } else if (kind == MG_ENT_GOAL) {
-        mg_transform_tr(AT(S.ex, ent), AT(S.ey, ent), 0.0, xf[MG_XF_MAIN]);
+    } else if (kind == MG_ENT_BLOCK && x == MG_XF_MAIN) {
+        const int b = AT(S.ebody0, ent);
+        body_sincos(S, e, b, s, c);
+        mg_transform_tr_sc(AT(S.bpx, b), AT(S.bpy, b), s, c, xf);
+    } else if (kind == MG_ENT_GOAL && x == MG_XF_MAIN) {
+        mg_transform_tr(AT(S.ex, ent), AT(S.ey, ent), 0.0, xf);
     }
 }
 
@@ -397,8 +412,9 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     if (view == 1 && tid == 32) {
         // Viewer.set_cam_follow / ego_cam_matrix: P @ (scale @ (tr1 @ (rot @ tr2)))
         int rb = S.robot_body0[e];
-        double rot[9], tr2[9], m1[9], m2[9], m3[9];
-        mg_transform_tr(0.0, 0.0, -AT(S.ba, rb), rot);
+        double rot[9], tr2[9], m1[9], m2[9], m3[9], sn, cs;
+        body_sincos(S, e, rb, sn, cs); // sincos(-a) = (-sin a, cos a): a correctly rounded sin is odd
+        mg_transform_tr_sc(0.0, 0.0, -sn, cs, rot);
         mg_transform_tr(-AT(S.bpx, rb), -AT(S.bpy, rb), 0.0, tr2);
         mg_mat3_mul(rot, tr2, m1);
         mg_mat3_mul(L->ego_tr1_m, m1, m2);
@@ -407,7 +423,8 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
         mg_mat3_mul(I3, m1, sm.u.pre.view);
     }
-    if (tid >= 64 && tid - 64 < nents) entity_xforms(S, e, tid - 64, sm.u.pre.e_xf[tid - 64]);
+    if (tid >= 64 && tid - 64 < 5 * nents)
+        entity_xform(S, e, (tid - 64) / 5, (tid - 64) % 5, sm.u.pre.e_xf[(tid - 64) / 5][(tid - 64) % 5]);
     RG_SYNC();
     if (tid == 0) {
         for (int k = 0; k < nents; k++) sm.e_g0[k + 1] += sm.e_g0[k];
@@ -576,7 +593,9 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     const bool keep_ring = stacked || (pp == MG_PREPROC_LORES3EA && view == 1);
     uint8_t *o_plain = view == 0 ? out.obs_allo : out.obs_ego;
     uint8_t *o_stack = pp == MG_PREPROC_LORESSTACK ? o_plain : out.obs_past;
-    const int oyl = tid / MG_LORES, ox = tid % MG_LORES, x0 = 4 * ox;
+    // 4x4 block of this thread: wave w covers block columns [32w, 32w + 32) of both block rows, so a
+    // geom's x-range meets few waves and the per-geom fill test is skipped wave-wide elsewhere
+    const int oyl = lane >> 5, ox = 32 * (tid >> 6) + (lane & 31), x0 = 4 * ox, lpix = oyl * MG_LORES + ox;
     // frame-stack threads (4 pixels each) hold frames t-3..t-1 of their pixels in registers
     const bool do_pf = mode == 0 && stacked && !fresh && tid < 2 * MG_LORES / 4;
 #ifdef MG_PROFILE
@@ -730,7 +749,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             (void)ya;
             uint64_t sum = 0;
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
+            for (int r = 0; r < ((dskip & 32) ? 0 : 4); r++) {
                 const uint4 lv = *(const uint4 *)&sm.u.post.band[yb + r][x0];
                 o[r][0] = o[r][0] > lv.x ? o[r][0] : lv.x;
                 o[r][1] = o[r][1] > lv.y ? o[r][1] : lv.y;
@@ -748,10 +767,10 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
                     }
                 }
             } else {
-                for (int ch = 0; ch < 3; ch++) {
+                for (int ch = 0; ch < ((dskip & 256) ? 0 : 3); ch++) {
                     const int ss = (int)((sum >> (16 * ch)) & 0xFFFF);
                     const int q = ss >> 4, rm = ss & 15;
-                    lo8[tid * 3 + ch] = (uint8_t)(q + (rm > 8 || (rm == 8 && (q & 1))));
+                    lo8[lpix * 3 + ch] = (uint8_t)(q + (rm > 8 || (rm == 8 && (q & 1))));
                 }
             }
         }
@@ -767,7 +786,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         // next band's empty spans, cleared outline layer, band list (wave 2) and prefetch
         for (int i = tid; i < nbl * RG_BAND; i += RG_THREADS)
             (&sm.bspan[0][0])[i] = (uint32_t)RG_EMPTY | ((uint32_t)RG_EMPTY << 16);
-        for (int i = tid; i < RG_BAND * MG_RES / 4; i += RG_THREADS)
+        for (int i = tid; i < ((dskip & 128) ? 0 : RG_BAND * MG_RES / 4); i += RG_THREADS)
             ((uint4 *)&sm.u.post.band[0][0])[i] = make_uint4(0, 0, 0, 0);
         if (tid == 0) sm.nlong = 0;
         if (mode == 0 && !(dskip & 4)) {
@@ -783,7 +802,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
                         *(uint4 *)(o_plain + (size_t)e * FR + lrow + 16 * c) = sm.u.post.lo[c];
                     }
                 }
-            } else if (stacked && tid < 2 * MG_LORES / 4) {
+            } else if (stacked && tid < 2 * MG_LORES / 4 && !(dskip & 64)) {
                 // FlattenFrameStack: [96][96][12] = frames oldest..newest concatenated per pixel; one thread
                 // per 4 pixels: 3 dwords of each frame in, 12 dwords (3 x 16 B) out
                 const uint32_t *c32 = (const uint32_t *)sm.u.post.lo;

@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for P in "$@"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $P -d "$OUT/p$i" -o run -- \
+  timeout -s KILL 120 rocprofv3 --pmc $P -d "$OUT/p$i" -o run -- \
     python "$R/bench.py" --no-cpu-baseline --steps 3 --warmup 1 > "$OUT/p$i.log" 2>&1
   rc=$?; echo "pass $i rc=$rc"
   [ $rc -eq 0 ] || { tail -20 "$OUT/p$i.log"; exit $rc; }
