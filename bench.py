@@ -25,7 +25,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
 
 
 def obs_bytes(preproc):
-    return {"LoRes4E": 165888, "LoRes4A": 165888, "LoResStack": 221184}.get(preproc, 2 * 384 * 384 * 3)
+    return {"LoRes4E": 165888, "LoRes4A": 165888, "LoRes3EA": 165888, "LoResCHW4E": 165888, "LoResCHW4A": 165888,
+            "LoResStack": 221184}.get(preproc, 2 * 384 * 384 * 3)
 
 
 def _cpu_worker(args):
@@ -59,14 +60,18 @@ def cpu_baseline(name, workers, steps):
             "per_core_env_steps_s": round(sum(r[0] / r[1] for r in res) / workers, 1)}
 
 
-def load_pmc(kernel):
+def load_pmc(kernel, workload, envs):
+    """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/pmc_traffic.json),
+    only when they were collected on this workload and env count."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         data = json.load(f)
     rec = data.get(kernel)
-    return rec["bytes_per_launch"] if rec else None
+    if not rec or rec.get("workload") != workload or rec.get("envs") != envs:
+        return None
+    return rec["bytes_per_launch"]
 
 
 def main():
@@ -77,7 +82,7 @@ def main():
     ap.add_argument("--envs", type=int, default=4096, help="env instances per GPU")
     ap.add_argument("--env", default="MoveToRegion-Demo-LoRes4E-v0")
     ap.add_argument("--cpu-workers", type=int, default=16)
-    ap.add_argument("--cpu-steps", type=int, default=1000)
+    ap.add_argument("--cpu-steps", type=int, default=1500)  # ~16 x 1 s of CPU work (about 15-25 s)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -140,7 +145,7 @@ def main():
         dom = "render_kernel" if t_render_ms >= t_step_ms else "step_kernel"
         dom_ms = max(t_render_ms, t_step_ms)
         achieved = per_env * n / (dom_ms * 1e-3) / 1e9
-        pmc = load_pmc(dom)
+        pmc = load_pmc(dom, args.env, n)
         out = {
             "metric": "env-steps/sec (whole node) at N instances/GPU, 1/2/4/8 MI355X",
             "value": round(value, 1),

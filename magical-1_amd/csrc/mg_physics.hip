@@ -69,11 +69,11 @@ __device__ __forceinline__ void carve_view(MGState &V, unsigned char *smem, cons
 // cp / acon / ahash blocks the HBM row of LDS row (k, r) is k * hcap + r
 template <typename T>
 __device__ __forceinline__ void xfer(T *lds, T *hbm, int rows, int blk, int lane, int N, int e, bool to_lds,
-                                     int groups = 1, int lcap = 0, int hcap = 0) {
+                                     int r0 = 0, int rs = 1, int groups = 1, int lcap = 0, int hcap = 0) {
 #pragma unroll 1
     for (int g = 0; g < groups; g++)
 #pragma unroll 2
-        for (int r = 0; r < rows; r++) {
+        for (int r = r0; r < rows; r += rs) {
             const uint32_t li = (uint32_t)(g * lcap + r) * blk + lane, hi = (uint32_t)(g * hcap + r) * N + e;
             if (to_lds) lds[li] = hbm[hi]; else hbm[hi] = lds[li];
         }
@@ -83,10 +83,12 @@ __device__ __forceinline__ void xfer(T *lds, T *hbm, int rows, int blk, int lane
 // bodies (incl. bias velocities and the rotation cache), the constraints' parameters and
 // warm-start impulses, the live arbiters (key, contacts, warm-start hashes) and the active list.
 // Cached shape BBs and the constraints' pre-step products are recomputed before use.
+// (r0, rs): rows r0, r0 + rs, ... of every array (rs = 64, r0 = lane: the cooperative form, one env per
+// wavefront, each lane a share of the rows)
 __device__ __forceinline__ void xfer_state(const MGState &S, const MGState &V, const StepCaps &c, int lane, int e,
-                                           bool in, bool cons_list = false) {
+                                           bool in, bool cons_list = false, int r0 = 0, int rs = 1) {
     const int blk = V.N, N = S.N;
-#define XF(f, rows) xfer(V.f, S.f, rows, blk, lane, N, e, in)
+#define XF(f, rows) xfer(V.f, S.f, rows, blk, lane, N, e, in, r0, rs)
 #define XS(f, r) do { if (in) V.f[(uint32_t)(r) * blk + lane] = S.f[(uint32_t)(r) * N + e]; \
                       else S.f[(uint32_t)(r) * N + e] = V.f[(uint32_t)(r) * blk + lane]; } while (0)
     XF(bpx, c.nb); XF(bpy, c.nb); XF(bvx, c.nb); XF(bvy, c.nb); XF(ba, c.nb); XF(bw, c.nb); XF(bvbx, c.nb);
@@ -97,13 +99,13 @@ __device__ __forceinline__ void xfer_state(const MGState &S, const MGState &V, c
         const bool need = in ? (k <= CP_JACC2 || (k >= 8 && k <= 11)) : (k == CP_JACC || k == CP_JACC2);
         if (!need) continue;
 #pragma unroll 2
-        for (int r = 0; r < c.nc; r++) {
+        for (int r = r0; r < c.nc; r += rs) {
             const uint32_t li = (uint32_t)(k * c.nc + r) * blk + lane, hi = (uint32_t)(k * MG_MAX_CONS + r) * N + e;
             if (in) V.cp[li] = S.cp[hi]; else S.cp[hi] = V.cp[li];
         }
     }
 #pragma unroll 1
-    for (int r = 0; r < c.na; r++) { // arbiter slots: only live ones carry data
+    for (int r = r0; r < c.na; r += rs) { // arbiter slots: only live ones carry data
         XS(akey, r);
         const int key = in ? V.akey[(uint32_t)r * blk + lane] : V.akey[(uint32_t)r * blk + lane];
         if (key < 0) continue;
@@ -119,9 +121,9 @@ __device__ __forceinline__ void xfer_state(const MGState &S, const MGState &V, c
         }
     }
     XF(nactive, 1);
-    const int nact = V.nactive[lane];
+    const int nact = in ? S.nactive[e] : V.nactive[lane];
 #pragma unroll 1
-    for (int r = 0; r < nact; r++) XS(active, r);
+    for (int r = r0; r < nact; r += rs) XS(active, r);
     XF(curr_dt, 1); XF(stamp, 1); XF(overflow, 1);
     if (in) { // read-only during the substeps
         XF(target_speed, 1); XF(rel_turn, 1); XF(target_finger, 1);
@@ -140,6 +142,7 @@ __host__ __device__ constexpr StepCaps step_variant_caps(int v) {
     return v == 1 ? StepCaps{6, 5, 10, 20, 16}    // robot only (MoveToRegion)
          : v == 2 ? StepCaps{7, 6, 12, 32, 16}    // robot + one single-shape block (MoveToCorner)
          : v == 3 ? StepCaps{14, 53, 26, 48, 1}   // up to 8 blocks incl. stars (Cluster*, MatchRegions): runtime lists
+         : v == 4 ? StepCaps{14, 53, 26, 48, 1}   // the same scenes, one env per 64-lane wavefront (cooperative)
          : StepCaps{0, 0, 0, 0, 0};
 }
 
@@ -163,6 +166,19 @@ __device__ __forceinline__ void env_substeps(const MGState &V, const mg_library 
     }
 }
 
+// the same with one env per wavefront: lane 0 drives the robot, every lane takes part in the step
+__device__ __forceinline__ void env_substeps_coop(const MGState &V, const mg_library *L, int lane, int a, MGProf &P) {
+    if (lane == 0) robot_set_action(V, L, 0, a < 18 ? a : 0);
+    const double dt = L->dt;
+    for (int i = 0; i < 10; i++) {
+        __syncthreads();
+        if (lane == 0) robot_update(V, L, 0);
+        __syncthreads();
+        MG_PP(P, 0);
+        space_step_coop(V, L, dt, lane, P);
+    }
+}
+
 template <int VAR, int BLK>
 __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg, int max_steps,
                                                   int auto_reset, const uint8_t *__restrict__ actions, float *reward,
@@ -170,8 +186,10 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr StepCaps C = step_variant_caps(VAR);
     constexpr bool LDS = VAR != 0;
-    constexpr int NCS = VAR == 3 ? 0 : C.nc; // compile-time constraint list (0: the env's runtime list)
-    const int lane = BLK == 1 ? 0 : threadIdx.x, e = xcd_block(blockIdx.x, gridDim.x) * BLK + lane;
+    constexpr bool COOP = VAR == 4;          // one env per workgroup of 64 lanes
+    constexpr int NCS = VAR >= 3 ? 0 : C.nc; // compile-time constraint list (0: the env's runtime list)
+    const int lane = COOP ? (int)threadIdx.x : BLK == 1 ? 0 : (int)threadIdx.x;
+    const int e = xcd_block(blockIdx.x, gridDim.x) * BLK + (COOP ? 0 : lane);
     if (e >= S.n_envs) return;
     const int a = actions[e];
     MGProf P;
@@ -196,9 +214,18 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
         // access through it compiles to ds_* with a constant offset from the lane's column
         MGState V = S;
         carve_view(V, smem, C, BLK);
-        xfer_state(S, V, C, lane, e, true, NCS == 0);
-        env_substeps<NCS>(V, L, lane, a, P);
-        xfer_state(S, V, C, lane, e, false);
+        if constexpr (COOP) {
+            xfer_state(S, V, C, 0, e, true, true, lane, 64);
+            __syncthreads();
+            env_substeps_coop(V, L, lane, a, P);
+            xfer_state(S, V, C, 0, e, false, true, lane, 64);
+            __syncthreads();
+            if (lane != 0) return;
+        } else {
+            xfer_state(S, V, C, lane, e, true, NCS == 0);
+            env_substeps<NCS>(V, L, lane, a, P);
+            xfer_state(S, V, C, lane, e, false);
+        }
     } else {
         env_substeps<0>(S, L, e, a, P);
     }
@@ -272,7 +299,7 @@ static hipError_t launch_step_var(const MGState &S, const mg_library *L, TaskCfg
         if (err != hipSuccess) return err;
         attr_set = true;
     }
-    hipLaunchKernelGGL((step_kernel<VAR, BLK>), dim3((S.n_envs + BLK - 1) / BLK), dim3(BLK), lds, st, S, L, cfg,
+    hipLaunchKernelGGL((step_kernel<VAR, BLK>), dim3((S.n_envs + BLK - 1) / BLK), dim3(VAR == 4 ? 64 : BLK), lds, st, S, L, cfg,
                        max_steps, auto_reset, actions, reward, done, eval_score, reset_mask);
     return hipGetLastError();
 }
@@ -281,6 +308,7 @@ static hipError_t launch_step_var(const MGState &S, const mg_library *L, TaskCfg
 bool mg_step_blk_ok(int variant, int blk) {
     return variant == 0 ? (blk == 1 || blk == 8 || blk == 64)
          : variant == 3 ? (blk == 1 || blk == 4)
+         : variant == 4 ? blk == 1
          : (blk == 1 || blk == 4 || blk == 16);
 }
 
@@ -292,7 +320,7 @@ hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, in
         return launch_step_var<V, B>(S, L, cfg, max_steps, auto_reset, actions, reward, done, eval_score, reset_mask, st);
     MG_STEP_CASE(1, 1) MG_STEP_CASE(1, 4) MG_STEP_CASE(1, 16)
     MG_STEP_CASE(2, 1) MG_STEP_CASE(2, 4) MG_STEP_CASE(2, 16)
-    MG_STEP_CASE(3, 1) MG_STEP_CASE(3, 4)
+    MG_STEP_CASE(3, 1) MG_STEP_CASE(3, 4) MG_STEP_CASE(4, 1)
     MG_STEP_CASE(0, 1) MG_STEP_CASE(0, 8) MG_STEP_CASE(0, 64)
 #undef MG_STEP_CASE
     return hipErrorInvalidValue;

@@ -180,21 +180,26 @@ static StepCaps step_caps(int task, int flags, int n_envs, const mg_library &lib
 }
 
 // Step kernel per scene (measured on MI355X, 8192 envs, ms per env-step of physics):
-// * compiled constraint lists (robot only / robot + one block): LDS variants 1/2, 16 envs per workgroup;
-// * MatchRegions (1-8 blocks, random per env): LDS variant 3, one env per workgroup, 10.6 ms vs
-//   21.1 ms for the HBM-state kernel, whose 64-env wavefronts diverge on the per-env scene;
-// * Cluster* (8-10 blocks in every env, dense contacts): the HBM-state kernel, 10.7 ms vs 15.1 ms
-//   for variant 3, which fits 8 envs per CU in LDS (19 KB each) and needs 4 rounds of workgroups.
+// * compiled constraint lists (robot only / robot + one block): LDS variants 1/2, 16 envs per workgroup,
+//   one env per lane;
+// * every other scene (up to 8 blocks, runtime constraint lists): the cooperative LDS variant 4, one env
+//   per 64-lane wavefront with the order-free parts across lanes -- MatchRegions-TestAll 6.0 ms (variant
+//   3, one env per single-lane workgroup: 10.6; HBM-state kernel, 64 envs per wavefront: 21.1),
+//   ClusterColour-Demo 8.6 ms (variant 3: 15.1; HBM-state kernel: 10.7).
 static int pick_step_variant(const StepCaps &c, int n_envs, int task) {
+    (void)task;
     int v = mg_step_variant(c, n_envs);
-    if (v == 3 && (task == MG_TASK_CLUSTER_COLOUR || task == MG_TASK_CLUSTER_SHAPE)) v = 0;
-    const char *ov = getenv("MG_STEP_VARIANT"); // experiments: force 0 (HBM) or a compiled variant
-    if (ov) { int w = atoi(ov); if (w == 0 || w == mg_step_variant(c, n_envs)) v = w; }
+    if (v == 3) v = 4;
+    const char *ov = getenv("MG_STEP_VARIANT");
+    if (ov) { // experiments: 0 (HBM state), the scene's compiled variant, or 3 <-> 4 (LDS runtime lists)
+        const int w = atoi(ov), base = mg_step_variant(c, n_envs);
+        if (w == 0 || w == base || (base == 3 && w == 4)) v = w;
+    }
     return v;
 }
 
 static int pick_step_blk(int variant) {
-    int b = variant == 0 ? 64 : variant == 3 ? 1 : 16;
+    int b = variant == 0 ? 64 : variant >= 3 ? 1 : 16;
     const char *ov = getenv(variant == 0 ? "MG_STEP_BLK0" : "MG_STEP_BLK"); // experiments
     if (ov && mg_step_blk_ok(variant, atoi(ov))) b = atoi(ov);
     return b;

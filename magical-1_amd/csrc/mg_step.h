@@ -729,6 +729,151 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
     MG_PP(P, 6);
 }
 
+// ---- cooperative cpSpaceStep: one env per wavefront ---------------------------
+// The env's state is an LDS view (N = 1, e = 0) shared by the 64 lanes of its wavefront.  The
+// order-free parts run across lanes: position integration and rotation caches (one body per lane),
+// shape BBs, the broadphase BB tests and narrowphase of all candidate pairs (one pair per lane, in
+// chunks of 64 pairs in canonical order), the stale-arbiter filter and the pre-steps of arbiters and
+// constraints.  Everything whose result depends on order runs on lane 0 in the serial code's order:
+// arbiter updates (pairs taken from the lanes in canonical pair order, so arbiter slots, the active
+// list and warm starts are those of space_step), the springs' pre-step impulses, applyCachedImpulse
+// and the 10 solver iterations.
+MG_DEV double rl_d(double v, int src) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), src);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+MG_DEV uint64_t rl_u64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// first pair index of shape i's row: for each shape i the 4 walls, then shapes j > i
+MG_DEV int pair_row_off(int i, int ns) { return i * (ns + 3) - (i * (i - 1)) / 2; }
+
+MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, int lane, MGProf &P) {
+    const int e = 0;
+    const uint32_t stamp = S.stamp[e] + 1;
+    const double prev_dt = S.curr_dt[e];
+    const int nact0 = S.nactive[e], nb = S.nbodies[e], ns = S.nshapes[e];
+    __syncthreads();
+    if (lane == 0) {
+        S.stamp[e] = stamp;
+        S.curr_dt[e] = dt;
+        for (int i = 0; i < nact0; i++) AT(S.astate, AT(S.active, i)) = ARB_NORMAL;
+        S.nactive[e] = 0;
+    }
+    for (int b = lane; b < nb; b += 64) {
+        AT(S.bpx, b) = AT(S.bpx, b) + (AT(S.bvx, b) + AT(S.bvbx, b)) * dt;
+        AT(S.bpy, b) = AT(S.bpy, b) + (AT(S.bvy, b) + AT(S.bvby, b)) * dt;
+        body_set_angle(S, e, b, AT(S.ba, b) + (AT(S.bw, b) + AT(S.bwb, b)) * dt);
+        AT(S.bvbx, b) = 0.0; AT(S.bvby, b) = 0.0; AT(S.bwb, b) = 0.0;
+    }
+    __syncthreads();
+    for (int k = lane; k < ns; k += 64) shape_update_bb(S, L, e, k);
+    __syncthreads();
+    MG_PP(P, 1);
+    // broadphase + narrowphase: pair p (canonical order) on lane p mod 64
+    const int total = pair_row_off(ns, ns);
+    for (int base = 0; base < total; base += 64) {
+        const int p = base + lane;
+        int i = 0, j = 0;
+        Collision info;
+        info.count = 0;
+        if (p < total) {
+            int lo = 0, hi = ns - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (pair_row_off(mid, ns) <= p) lo = mid; else hi = mid - 1;
+            }
+            i = lo;
+            const int r = p - pair_row_off(i, ns);
+            const double al = AT(S.sbbl, i), ab = AT(S.sbbb, i), ar = AT(S.sbbr, i), at = AT(S.sbbt, i);
+            if (r < 4) {
+                j = -1 - r;
+                double wl, wb, wr, wt;
+                wall_bb(r, wl, wb, wr, wt);
+                if (al <= wr && wl <= ar && ab <= wt && wb <= at) {
+                    ShapeW A, W;
+                    load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A);
+                    load_wall(r, W);
+                    collide(A, W, info);
+                }
+            } else {
+                j = i + 1 + (r - 4);
+                const int gi = AT(S.sgroup, i), gj = AT(S.sgroup, j);
+                if (al <= AT(S.sbbr, j) && AT(S.sbbl, j) <= ar && ab <= AT(S.sbbt, j) && AT(S.sbbb, j) <= at &&
+                    AT(S.sbody, j) != AT(S.sbody, i) && !(gi != 0 && gi == gj)) {
+                    ShapeW A, B;
+                    load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A);
+                    load_shape(S, L, e, j, (uint64_t)AT(S.shash, j), B);
+                    collide(A, B, info);
+                }
+            }
+        }
+        uint64_t m = __ballot(info.count > 0);
+        while (m) { // hits in lane order = canonical pair order
+            const int src = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            Collision c;
+            c.count = __builtin_amdgcn_readlane(info.count, src);
+            c.n = v2(rl_d(info.n.x, src), rl_d(info.n.y, src));
+            for (int k = 0; k < 2; k++) {
+                c.p1[k] = v2(rl_d(info.p1[k].x, src), rl_d(info.p1[k].y, src));
+                c.p2[k] = v2(rl_d(info.p2[k].x, src), rl_d(info.p2[k].y, src));
+                c.hash[k] = rl_u64(info.hash[k], src);
+            }
+            const int si = __builtin_amdgcn_readlane(i, src), sj = __builtin_amdgcn_readlane(j, src);
+            if (lane == 0) {
+                ShapeW A, B; // arbiter_update reads the shapes' types and bodies only
+                A.type = AT(S.spoly, si) < 0 ? WS_CIRCLE : WS_POLY;
+                A.body = AT(S.sbody, si);
+                double ub;
+                int key;
+                if (sj < 0) {
+                    B.type = WS_SEGMENT; B.body = -1; ub = 0.8; key = si * 128 + 100 + (-1 - sj);
+                } else {
+                    B.type = AT(S.spoly, sj) < 0 ? WS_CIRCLE : WS_POLY; B.body = AT(S.sbody, sj);
+                    ub = AT(S.su, sj); key = si * 128 + sj;
+                }
+                arbiter_update(S, L, e, key, A, B, AT(S.su, si), ub, c);
+            }
+        }
+    }
+    __syncthreads();
+    MG_PP(P, 2);
+    for (int i = lane; i < S.arb_cap; i += 64) { // cached arbiter filter
+        if (AT(S.akey, i) < 0) continue;
+        const uint32_t ticks = stamp - AT(S.astamp, i);
+        if (ticks >= 1 && AT(S.astate, i) != ARB_CACHED) AT(S.astate, i) = ARB_CACHED;
+        if (ticks >= 3) { AT(S.akey, i) = -1; AT(S.acount, i) = 0; }
+    }
+    __syncthreads();
+    MG_PP(P, 3);
+    const int nact = S.nactive[e], nc = S.ncons[e];
+    for (int i = lane; i < nact; i += 64) arbiter_prestep(S, L, e, AT(S.active, i), dt);
+    for (int c = lane; c < nc; c += 64)
+        if (AT(S.ctype, c) != MG_C_SPRING) cons_prestep(S, e, c, dt); // touch only their own terms
+    __syncthreads();
+    if (lane == 0) {
+        for (int c = 0; c < nc; c++) // the springs apply their impulses to body velocities: in order
+            if (AT(S.ctype, c) == MG_C_SPRING) cons_prestep(S, e, c, dt);
+        MG_PP(P, 4);
+        const double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
+        for (int i = 0; i < nact; i++) arbiter_cached(S, e, AT(S.active, i), dt_coef);
+        for (int c = 0; c < nc; c++) cons_cached(S, e, c, dt_coef);
+        MG_PP(P, 5);
+        for (int it = 0; it < 10; it++) {
+            for (int i = 0; i < nact; i++) arbiter_apply(S, e, AT(S.active, i));
+            for (int c = 0; c < nc; c++) cons_apply(S, e, c, dt);
+        }
+        MG_PP(P, 6);
+    }
+    __syncthreads();
+}
+
 // ---- robot control ---------------------------------------------------------
 MG_DEV void robot_set_action(const MGState &S, const mg_library *L, int e, int action) {
     const int ud = action % 3, lr = (action / 3) % 3;

@@ -115,7 +115,8 @@ def test_rollout_parity(name, n, steps):
 
 
 # every compiled step-kernel form, forced through the experiment switches read at mg_create
-# (MG_STEP_VARIANT: 0 = HBM state, 1/2 = compile-time constraint lists, 3 = LDS with runtime lists;
+# (MG_STEP_VARIANT: 0 = HBM state, 1/2 = compile-time constraint lists, 3 = LDS with runtime lists and
+# one env per single-lane workgroup, 4 (default for those scenes) = the same one env per 64-lane wavefront;
 # MG_STEP_BLK / MG_STEP_BLK0: envs per workgroup)
 KERNEL_FORMS = [
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_BLK": "1"}),
@@ -125,6 +126,8 @@ KERNEL_FORMS = [
     ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "1"}),
     ("ClusterColour-Demo-LoResStack-v0", 66, 30, {"MG_STEP_VARIANT": "3", "MG_STEP_BLK": "1"}),
     ("ClusterColour-Demo-LoResStack-v0", 66, 30, {"MG_STEP_VARIANT": "3", "MG_STEP_BLK": "4"}),
+    ("FindDupe-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "3"}),
+    ("ClusterShape-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0"}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0"}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "8"}),
 ]

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--md", action="store_true")
     ap.add_argument("--traffic-json")
     ap.add_argument("--kernel", default="render_kernel")
+    ap.add_argument("--workload", default="MoveToRegion-Demo-LoRes4E-v0")
+    ap.add_argument("--envs", type=int, default=4096)
     a = ap.parse_args()
     out = []
     for db in sorted(glob.glob(os.path.join(a.dir, "**", "*.db"), recursive=True)):
@@ -66,7 +68,7 @@ def main():
             data = json.load(open(a.traffic_json))
         if fetch is not None and write is not None:
             data[a.kernel] = {"bytes_per_launch": round(fetch + write), "read_bytes": round(fetch),
-                              "write_bytes": round(write), "source": a.dir,
+                              "write_bytes": round(write), "source": a.dir, "workload": a.workload, "envs": a.envs,
                               "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->B"}
             json.dump(data, open(a.traffic_json, "w"), indent=1)
             print("traffic", a.kernel, data[a.kernel])
