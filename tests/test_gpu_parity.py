@@ -502,3 +502,33 @@ def test_sb3_vec_env(name):
                 assert "terminal_observation" not in infos[i]
                 ref[i] = last
     venv.close()
+
+
+@pytest.mark.gpu
+def test_batched_evaluation_protocol():
+    """BatchedEvaluationProtocol: each test variant's n_rollouts episodes run as one GPU batch; every
+    score equals the oracle episode driven by the same actions."""
+    from magical_amd import evaluation
+    n = 6
+    recorded = []
+
+    def policy(obs):
+        a = torch.as_tensor(np.random.RandomState(len(recorded)).randint(0, 18, n), dtype=torch.uint8).cuda()
+        recorded.append(a.cpu().numpy())
+        return a
+
+    class Checked(evaluation.BatchedEvaluationProtocol):
+        def obtain_scores(self, env_name):
+            recorded.clear()
+            scores = super().obtain_scores(env_name)
+            spec = registry.lookup(env_name)
+            for i in range(n):
+                o = po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, spec.max_episode_steps, seed=i)
+                o.reset()
+                for t, acts in enumerate(recorded):
+                    _, _, d, s = o.step(int(acts[i]))
+                assert d and s == scores[i], (env_name, i)
+            return scores
+
+    frame = Checked("MoveToRegion-Demo-LoRes4E-v0", n, policy, run_id="random").do_eval()
+    assert len(frame) == 1 + len(registry.DEMO_ENVS_TO_TEST_ENVS_MAP["MoveToRegion-Demo-LoRes4E-v0"])

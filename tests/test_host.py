@@ -183,3 +183,42 @@ def test_two_rank_gloo_sharded_rollout_equals_single_process(tmp_path):
     for t in range(6):
         ref = np.stack([e.step(int(a))[0] for e, a in zip(envs, acts[t])])
     assert np.array_equal(full, ref)
+
+
+# --------------------------------------------------------------------------- evaluation protocol
+def test_evaluation_protocol_statistics():
+    """evaluation.py:13-98: one record per test env of the demo env, mean / t-CI / std (ddof=1),
+    extra scores truncated with a warning, too few scores rejected."""
+    import warnings
+    import numpy as np
+    from scipy import stats
+    from magical_amd import evaluation
+
+    rs = np.random.RandomState(0)
+    table = {}
+
+    class Fixed(evaluation.EvaluationProtocol):
+        run_id = "fixed"
+
+        def obtain_scores(self, env_name):
+            return table.setdefault(env_name, rs.rand(self.n_rollouts + 2).tolist())
+
+    proto = Fixed("MoveToCorner-Demo-v0", 10)
+    assert proto.test_env_names[0] == "MoveToCorner-Demo-v0" and len(proto.test_env_names) == 6
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        frame = proto.do_eval()
+    assert len(w) == len(proto.test_env_names)
+    assert list(frame["test_env"]) == proto.test_env_names
+    for _, row in frame.iterrows():
+        s = np.asarray(table[row["test_env"]][:10])
+        lo, hi = stats.t.interval(0.95, len(s) - 1, loc=s.mean(), scale=stats.sem(s))
+        assert np.isclose(row["mean_score"], s.mean()) and np.isclose(row["std_score"], s.std(ddof=1))
+        assert np.isclose(row["ci95_lower"], lo) and np.isclose(row["ci95_upper"], hi)
+
+    class Short(Fixed):
+        def obtain_scores(self, env_name):
+            return [0.5] * 3
+    import pytest
+    with pytest.raises(ValueError):
+        Short("MoveToCorner-Demo-v0", 10).do_eval()
