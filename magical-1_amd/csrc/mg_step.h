@@ -753,6 +753,178 @@ MG_DEV uint64_t rl_u64(uint64_t v, int src) {
 // first pair index of shape i's row: for each shape i the 4 walls, then shapes j > i
 MG_DEV int pair_row_off(int i, int ns) { return i * (ns + 3) - (i * (i - 1)) / 2; }
 
+// The serial sweep of the cooperative step keeps the body velocities in the wavefront's VGPRs, spread
+// over the lanes (lane b holds body b): every lane runs the sweep on the same (uniform) values, reading
+// a body with readlane by its wave-uniform slot and writing it with a lane-select, so no body state
+// makes an LDS round trip.  Same operations in the same order as cons_*_impl / arbiter_*.
+struct LaneBodies { double vx, vy, w, vbx, vby, wb, minv, iinv; };
+MG_DEV int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
+MG_DEV double lget(double f, int b) { return b < 0 ? 0.0 : rl_d(f, b); }
+MG_DEV void lput(double &f, int b, int lane, double v) { f = lane == b ? v : f; }
+MG_DEV void lapply(LaneBodies &R, int lane, int b, V2 j, V2 r) {
+    if (b < 0) return;
+    const double minv = lget(R.minv, b), iinv = lget(R.iinv, b);
+    lput(R.vx, b, lane, lget(R.vx, b) + j.x * minv);
+    lput(R.vy, b, lane, lget(R.vy, b) + j.y * minv);
+    lput(R.w, b, lane, lget(R.w, b) + iinv * vcross(r, j));
+}
+MG_DEV void lapply_bias(LaneBodies &R, int lane, int b, V2 j, V2 r) {
+    if (b < 0) return;
+    const double minv = lget(R.minv, b), iinv = lget(R.iinv, b);
+    lput(R.vbx, b, lane, lget(R.vbx, b) + j.x * minv);
+    lput(R.vby, b, lane, lget(R.vby, b) + j.y * minv);
+    lput(R.wb, b, lane, lget(R.wb, b) + iinv * vcross(r, j));
+}
+MG_DEV void ladd_w(LaneBodies &R, int lane, int b, double dw) { // AT(S.bw, b) += dw
+    if (b >= 0) lput(R.w, b, lane, lget(R.w, b) + dw);
+}
+MG_DEV void lsub_w(LaneBodies &R, int lane, int b, double dw) { // AT(S.bw, b) -= dw
+    if (b >= 0) lput(R.w, b, lane, lget(R.w, b) - dw);
+}
+
+MG_DEV void lcons_cached(LaneBodies &R, int lane, const MGState &S, int e, int c, int a, int b, int type,
+                         double dt_coef) {
+    switch (type) {
+    case MG_C_PIVOT: {
+        V2 j = vmult(v2(CPA(CP_JACC, c), CPA(CP_JACC2, c)), dt_coef);
+        lapply(R, lane, a, vneg(j), v2(CPA(CP_R1X, c), CPA(CP_R1Y, c)));
+        lapply(R, lane, b, j, v2(CPA(CP_R2X, c), CPA(CP_R2Y, c)));
+        break;
+    }
+    case MG_C_GEAR: {
+        double j = CPA(CP_JACC, c) * dt_coef;
+        lsub_w(R, lane, a, j * lget(R.iinv, a) * CPA(CP_RATIO_INV, c));
+        ladd_w(R, lane, b, j * lget(R.iinv, b));
+        break;
+    }
+    case MG_C_ROTLIMIT:
+    case MG_C_MOTOR: {
+        double j = CPA(CP_JACC, c) * dt_coef;
+        lsub_w(R, lane, a, j * lget(R.iinv, a));
+        ladd_w(R, lane, b, j * lget(R.iinv, b));
+        break;
+    }
+    default: break;
+    }
+}
+
+MG_DEV void lcons_apply(LaneBodies &R, int lane, const MGState &S, int e, int c, int a, int b, int type, double dt) {
+    switch (type) {
+    case MG_C_PIVOT: {
+        V2 r1 = v2(CPA(CP_R1X, c), CPA(CP_R1Y, c)), r2 = v2(CPA(CP_R2X, c), CPA(CP_R2Y, c));
+        V2 v1 = vadd(v2(lget(R.vx, a), lget(R.vy, a)), vmult(vperp(r1), lget(R.w, a)));
+        V2 v2_ = vadd(v2(lget(R.vx, b), lget(R.vy, b)), vmult(vperp(r2), lget(R.w, b)));
+        V2 vr = vsub(v2_, v1);
+        V2 d = vsub(v2(CPA(CP_BIAS, c), CPA(CP_BIAS2, c)), vr);
+        V2 j = v2(d.x * CPA(CP_K11, c) + d.y * CPA(CP_K12, c), d.x * CPA(CP_K21, c) + d.y * CPA(CP_K22, c));
+        V2 jOld = v2(CPA(CP_JACC, c), CPA(CP_JACC2, c));
+        V2 jAcc = vclamp(vadd(jOld, j), CPA(CP_MAXF, c) * dt);
+        if (lane == 0) { CPA(CP_JACC, c) = jAcc.x; CPA(CP_JACC2, c) = jAcc.y; }
+        V2 dj = vsub(jAcc, jOld);
+        lapply(R, lane, a, vneg(dj), r1);
+        lapply(R, lane, b, dj, r2);
+        break;
+    }
+    case MG_C_GEAR: {
+        double ratio = CPA(CP_RATIO, c);
+        double wr = lget(R.w, b) * ratio - lget(R.w, a);
+        double jMax = CPA(CP_MAXF, c) * dt;
+        double j = (CPA(CP_BIAS, c) - wr) * CPA(CP_ISUM, c);
+        double jOld = CPA(CP_JACC, c);
+        double jAcc = cpclamp(jOld + j, -jMax, jMax);
+        if (lane == 0) CPA(CP_JACC, c) = jAcc;
+        j = jAcc - jOld;
+        lsub_w(R, lane, a, j * lget(R.iinv, a) * CPA(CP_RATIO_INV, c));
+        ladd_w(R, lane, b, j * lget(R.iinv, b));
+        break;
+    }
+    case MG_C_ROTLIMIT: {
+        double bias = CPA(CP_BIAS, c);
+        if (!bias) return;
+        double wr = lget(R.w, b) - lget(R.w, a);
+        double jMax = CPA(CP_MAXF, c) * dt;
+        double j = -(bias + wr) * CPA(CP_ISUM, c);
+        double jOld = CPA(CP_JACC, c);
+        double jAcc = bias < 0.0 ? cpclamp(jOld + j, 0.0, jMax) : cpclamp(jOld + j, -jMax, 0.0);
+        if (lane == 0) CPA(CP_JACC, c) = jAcc;
+        j = jAcc - jOld;
+        lsub_w(R, lane, a, j * lget(R.iinv, a));
+        ladd_w(R, lane, b, j * lget(R.iinv, b));
+        break;
+    }
+    case MG_C_MOTOR: {
+        double wr = lget(R.w, b) - lget(R.w, a) + CPA(CP_RATE, c);
+        double jMax = CPA(CP_MAXF, c) * dt;
+        double j = -wr * CPA(CP_ISUM, c);
+        double jOld = CPA(CP_JACC, c);
+        double jAcc = cpclamp(jOld + j, -jMax, jMax);
+        if (lane == 0) CPA(CP_JACC, c) = jAcc;
+        j = jAcc - jOld;
+        lsub_w(R, lane, a, j * lget(R.iinv, a));
+        ladd_w(R, lane, b, j * lget(R.iinv, b));
+        break;
+    }
+    case MG_C_SPRING: {
+        double wrn = lget(R.w, a) - lget(R.w, b);
+        double w_damp = (CPA(CP_TWRN, c) - wrn) * CPA(CP_WCOEF, c);
+        double j_damp = w_damp * CPA(CP_ISUM, c);
+        double jacc = CPA(CP_JACC, c) + j_damp;
+        if (lane == 0) { CPA(CP_TWRN, c) = wrn + w_damp; CPA(CP_JACC, c) = jacc; }
+        ladd_w(R, lane, a, j_damp * lget(R.iinv, a));
+        lsub_w(R, lane, b, j_damp * lget(R.iinv, b));
+        break;
+    }
+    }
+}
+
+MG_DEV void larb_cached(LaneBodies &R, int lane, const MGState &S, int e, int slot, double dt_coef) {
+    if (ufirst(AT(S.astate, slot)) == ARB_FIRST) return;
+    const int a = ufirst(AT(S.asa, slot)), b = ufirst(AT(S.asb, slot));
+    V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
+    const int cnt = ufirst(AT(S.acount, slot));
+    for (int k = 0; k < cnt; k++) {
+        V2 j = vmult(vrotate(n, v2(ACON(k, AC_JN, slot), ACON(k, AC_JT, slot))), dt_coef);
+        lapply(R, lane, a, vneg(j), v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)));
+        lapply(R, lane, b, j, v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot)));
+    }
+}
+
+MG_DEV void larb_apply(LaneBodies &R, int lane, const MGState &S, int e, int slot) {
+    const int a = ufirst(AT(S.asa, slot)), b = ufirst(AT(S.asb, slot));
+    V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
+    double friction = AT(S.au, slot);
+    const int cnt = ufirst(AT(S.acount, slot));
+    for (int k = 0; k < cnt; k++) {
+        double nMass = ACON(k, AC_NMASS, slot);
+        V2 r1 = v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)), r2 = v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot));
+        V2 vb1 = vadd(v2(lget(R.vbx, a), lget(R.vby, a)), vmult(vperp(r1), lget(R.wb, a)));
+        V2 vb2 = vadd(v2(lget(R.vbx, b), lget(R.vby, b)), vmult(vperp(r2), lget(R.wb, b)));
+        V2 v1 = vadd(v2(lget(R.vx, a), lget(R.vy, a)), vmult(vperp(r1), lget(R.w, a)));
+        V2 v2_ = vadd(v2(lget(R.vx, b), lget(R.vy, b)), vmult(vperp(r2), lget(R.w, b)));
+        V2 vr = vsub(v2_, v1);
+        double vbn = vdot(vsub(vb2, vb1), n);
+        double vrn = vdot(vr, n);
+        double vrt = vdot(vr, vperp(n));
+        double jbn = (ACON(k, AC_BIAS, slot) - vbn) * nMass;
+        double jbnOld = ACON(k, AC_JB, slot);
+        double jBias = cpmax(jbnOld + jbn, 0.0);
+        double jn = -(0.0 + vrn) * nMass;
+        double jnOld = ACON(k, AC_JN, slot);
+        double jnAcc = cpmax(jnOld + jn, 0.0);
+        double jtMax = friction * jnAcc;
+        double jt = -vrt * ACON(k, AC_TMASS, slot);
+        double jtOld = ACON(k, AC_JT, slot);
+        double jtAcc = cpclamp(jtOld + jt, -jtMax, jtMax);
+        if (lane == 0) { ACON(k, AC_JB, slot) = jBias; ACON(k, AC_JN, slot) = jnAcc; ACON(k, AC_JT, slot) = jtAcc; }
+        V2 jb = vmult(n, jBias - jbnOld);
+        lapply_bias(R, lane, a, vneg(jb), r1);
+        lapply_bias(R, lane, b, jb, r2);
+        V2 j = vrotate(n, v2(jnAcc - jnOld, jtAcc - jtOld));
+        lapply(R, lane, a, vneg(j), r1);
+        lapply(R, lane, b, j, r2);
+    }
+}
+
 MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, int lane, MGProf &P) {
     const int e = 0;
     const uint32_t stamp = S.stamp[e] + 1;
@@ -857,20 +1029,35 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
     for (int c = lane; c < nc; c += 64)
         if (AT(S.ctype, c) != MG_C_SPRING) cons_prestep(S, e, c, dt); // touch only their own terms
     __syncthreads();
-    if (lane == 0) {
+    if (lane == 0)
         for (int c = 0; c < nc; c++) // the springs apply their impulses to body velocities: in order
             if (AT(S.ctype, c) == MG_C_SPRING) cons_prestep(S, e, c, dt);
-        MG_PP(P, 4);
-        const double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
-        for (int i = 0; i < nact; i++) arbiter_cached(S, e, AT(S.active, i), dt_coef);
-        for (int c = 0; c < nc; c++) cons_cached(S, e, c, dt_coef);
-        MG_PP(P, 5);
-        for (int it = 0; it < 10; it++) {
-            for (int i = 0; i < nact; i++) arbiter_apply(S, e, AT(S.active, i));
-            for (int c = 0; c < nc; c++) cons_apply(S, e, c, dt);
-        }
-        MG_PP(P, 6);
+    __syncthreads();
+    MG_PP(P, 4);
+    // applyCachedImpulse + 10 iterations with the bodies in the lanes' registers
+    LaneBodies R = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (lane < nb) {
+        R.vx = AT(S.bvx, lane); R.vy = AT(S.bvy, lane); R.w = AT(S.bw, lane);
+        R.vbx = AT(S.bvbx, lane); R.vby = AT(S.bvby, lane); R.wb = AT(S.bwb, lane);
+        R.minv = AT(S.bminv, lane); R.iinv = AT(S.biinv, lane);
     }
+    const double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
+    const int unact = ufirst(nact), unc = ufirst(nc);
+    for (int i = 0; i < unact; i++) larb_cached(R, lane, S, e, ufirst(AT(S.active, i)), dt_coef);
+    for (int c = 0; c < unc; c++)
+        lcons_cached(R, lane, S, e, c, ufirst(AT(S.ca, c)), ufirst(AT(S.cb, c)), ufirst(AT(S.ctype, c)), dt_coef);
+    MG_PP(P, 5);
+#pragma unroll 1
+    for (int it = 0; it < 10; it++) {
+        for (int i = 0; i < unact; i++) larb_apply(R, lane, S, e, ufirst(AT(S.active, i)));
+        for (int c = 0; c < unc; c++)
+            lcons_apply(R, lane, S, e, c, ufirst(AT(S.ca, c)), ufirst(AT(S.cb, c)), ufirst(AT(S.ctype, c)), dt);
+    }
+    if (lane < nb) {
+        AT(S.bvx, lane) = R.vx; AT(S.bvy, lane) = R.vy; AT(S.bw, lane) = R.w;
+        AT(S.bvbx, lane) = R.vbx; AT(S.bvby, lane) = R.vby; AT(S.bwb, lane) = R.wb;
+    }
+    MG_PP(P, 6);
     __syncthreads();
 }
 
