@@ -54,7 +54,14 @@ def cpu_baseline(name, workers, steps):
         res = pool.map(_cpu_worker, [(name, steps, 1000 + i) for i in range(workers)])
     wall = time.perf_counter() - t0
     total = sum(r[0] for r in res)
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), cpu_model)
+    except OSError:
+        pass
     return {"value": round(total / wall, 1), "unit": "env-steps/s", "cores": workers, "kind": "port",
+            "cpu_model": cpu_model, "host_cpus": os.cpu_count(),
             "sample": f"{workers} processes x 1 env x {steps} steps of {name} (C oracle restatement, "
                       f"1 env per core, incl. resets); wall {wall:.1f}s",
             "per_core_env_steps_s": round(sum(r[0] / r[1] for r in res) / workers, 1)}
