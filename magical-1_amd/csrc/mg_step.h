@@ -925,6 +925,74 @@ MG_DEV void larb_apply(LaneBodies &R, int lane, const MGState &S, int e, int slo
     }
 }
 
+// A block's ground joints (Pivot + Gear to the static body, entities.py:580-754) touch only the
+// block's body.  When no other constraint touches that body, they commute exactly with every other
+// constraint row of the sweep (disjoint bodies; the static body's velocity is never read or written),
+// so the lane holding the body applies them itself, in list order, while the rest of the constraint
+// list runs in the serial sweep: bit-identical to the serial order, with the 2 x nblocks ground rows
+// of an iteration costing two row evaluations instead of 2 x nblocks.
+struct GroundRows { int n, c0, c1; uint64_t mask; };
+MG_DEV GroundRows ground_rows(const MGState &S, int e, int lane, int nb, int nc) {
+    int n = 0, c0 = -1, c1 = -1;
+    bool bad = lane >= nb;
+    for (int c = 0; c < nc && !bad; c++) {
+        const int a = AT(S.ca, c), b = AT(S.cb, c), t = AT(S.ctype, c);
+        if (a != lane && b != lane) continue;
+        if (a < 0 && (t == MG_C_PIVOT || t == MG_C_GEAR) && n < 2) {
+            if (n == 0) c0 = c; else c1 = c;
+            n++;
+        } else {
+            bad = true;
+        }
+    }
+    GroundRows g;
+    g.n = bad ? 0 : n; g.c0 = c0; g.c1 = c1;
+    g.mask = __ballot(g.n > 0);
+    return g;
+}
+MG_DEV bool is_ground_row(const GroundRows &G, int b) { return b >= 0 && ((G.mask >> b) & 1ull); }
+
+// lcons_cached / lcons_apply of a ground row on the lane that holds body b (body a static)
+MG_DEV void lground_cached(LaneBodies &R, const MGState &S, int e, int c, double dt_coef) {
+    if (AT(S.ctype, c) == MG_C_PIVOT) {
+        V2 j = vmult(v2(CPA(CP_JACC, c), CPA(CP_JACC2, c)), dt_coef);
+        V2 r2 = v2(CPA(CP_R2X, c), CPA(CP_R2Y, c));
+        R.vx = R.vx + j.x * R.minv;
+        R.vy = R.vy + j.y * R.minv;
+        R.w = R.w + R.iinv * vcross(r2, j);
+    } else { // MG_C_GEAR
+        double j = CPA(CP_JACC, c) * dt_coef;
+        R.w = R.w + j * R.iinv;
+    }
+}
+MG_DEV void lground_apply(LaneBodies &R, const MGState &S, int e, int c, double dt) {
+    if (AT(S.ctype, c) == MG_C_PIVOT) {
+        V2 r1 = v2(CPA(CP_R1X, c), CPA(CP_R1Y, c)), r2 = v2(CPA(CP_R2X, c), CPA(CP_R2Y, c));
+        V2 v1 = vadd(v2(0.0, 0.0), vmult(vperp(r1), 0.0));
+        V2 v2_ = vadd(v2(R.vx, R.vy), vmult(vperp(r2), R.w));
+        V2 vr = vsub(v2_, v1);
+        V2 d = vsub(v2(CPA(CP_BIAS, c), CPA(CP_BIAS2, c)), vr);
+        V2 j = v2(d.x * CPA(CP_K11, c) + d.y * CPA(CP_K12, c), d.x * CPA(CP_K21, c) + d.y * CPA(CP_K22, c));
+        V2 jOld = v2(CPA(CP_JACC, c), CPA(CP_JACC2, c));
+        V2 jAcc = vclamp(vadd(jOld, j), CPA(CP_MAXF, c) * dt);
+        CPA(CP_JACC, c) = jAcc.x; CPA(CP_JACC2, c) = jAcc.y;
+        V2 dj = vsub(jAcc, jOld);
+        R.vx = R.vx + dj.x * R.minv;
+        R.vy = R.vy + dj.y * R.minv;
+        R.w = R.w + R.iinv * vcross(r2, dj);
+    } else { // MG_C_GEAR
+        double ratio = CPA(CP_RATIO, c);
+        double wr = R.w * ratio - 0.0;
+        double jMax = CPA(CP_MAXF, c) * dt;
+        double j = (CPA(CP_BIAS, c) - wr) * CPA(CP_ISUM, c);
+        double jOld = CPA(CP_JACC, c);
+        double jAcc = cpclamp(jOld + j, -jMax, jMax);
+        CPA(CP_JACC, c) = jAcc;
+        j = jAcc - jOld;
+        R.w = R.w + j * R.iinv;
+    }
+}
+
 MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, int lane, MGProf &P) {
     const int e = 0;
     const uint32_t stamp = S.stamp[e] + 1;
@@ -1043,15 +1111,30 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
     }
     const double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
     const int unact = ufirst(nact), unc = ufirst(nc);
+    const GroundRows G = ground_rows(S, e, lane, nb, nc);
     for (int i = 0; i < unact; i++) larb_cached(R, lane, S, e, ufirst(AT(S.active, i)), dt_coef);
-    for (int c = 0; c < unc; c++)
-        lcons_cached(R, lane, S, e, c, ufirst(AT(S.ca, c)), ufirst(AT(S.cb, c)), ufirst(AT(S.ctype, c)), dt_coef);
+    if (G.n > 0) {
+        lground_cached(R, S, e, G.c0, dt_coef);
+        if (G.n > 1) lground_cached(R, S, e, G.c1, dt_coef);
+    }
+    for (int c = 0; c < unc; c++) {
+        const int cb = ufirst(AT(S.cb, c));
+        if (is_ground_row(G, cb)) continue;
+        lcons_cached(R, lane, S, e, c, ufirst(AT(S.ca, c)), cb, ufirst(AT(S.ctype, c)), dt_coef);
+    }
     MG_PP(P, 5);
 #pragma unroll 1
     for (int it = 0; it < 10; it++) {
         for (int i = 0; i < unact; i++) larb_apply(R, lane, S, e, ufirst(AT(S.active, i)));
-        for (int c = 0; c < unc; c++)
-            lcons_apply(R, lane, S, e, c, ufirst(AT(S.ca, c)), ufirst(AT(S.cb, c)), ufirst(AT(S.ctype, c)), dt);
+        if (G.n > 0) {
+            lground_apply(R, S, e, G.c0, dt);
+            if (G.n > 1) lground_apply(R, S, e, G.c1, dt);
+        }
+        for (int c = 0; c < unc; c++) {
+            const int cb = ufirst(AT(S.cb, c));
+            if (is_ground_row(G, cb)) continue;
+            lcons_apply(R, lane, S, e, c, ufirst(AT(S.ca, c)), cb, ufirst(AT(S.ctype, c)), dt);
+        }
     }
     if (lane < nb) {
         AT(S.bvx, lane) = R.vx; AT(S.bvy, lane) = R.vy; AT(S.bw, lane) = R.w;
