@@ -3,13 +3,16 @@
 python bench.py --gpus N --steps K --warmup W [--envs 4096] [--env MoveToRegion-Demo-LoRes4E-v0]
 
 One env-step = one step() of every env: action decode, 10 physics substeps
-(Chipmunk-7 semantics), episode bookkeeping + score + in-place reset at the
-40-step episode boundary, allocentric + egocentric 384^2 render, 96^2 area
-downsample and LoRes4E frame stack.  Actions come from device Philox
-(key 42, counter = (step, env)).  Multi-GPU: one process per GPU, envs sharded
-contiguously (global env id = rank * envs + i, seed 1000 + id), no data-path
-collective (instances are independent) -> weak scaling; the timed region is
-bracketed by barrier + synchronize and the max over ranks is reported.
+(Chipmunk-7 semantics), episode bookkeeping + score, the in-place reset of the
+envs whose episode ended, allocentric + egocentric 384^2 render, 96^2 area
+downsample and LoRes4E frame stack.  Episode phases are staggered (env i starts
+at episode step i mod max_episode_steps; --no-phase-spread starts them in
+phase), so every timed step resets ~N / max_episode_steps envs, as a steady
+training stream does.  Actions come from device Philox (key 42, counter =
+(step, env)).  Multi-GPU: one process per GPU, envs sharded contiguously
+(global env id = rank * envs + i, seed 1000 + id), no data-path collective
+(instances are independent) -> weak scaling; the timed region is bracketed by
+barrier + synchronize and the max over ranks is reported.
 """
 import argparse
 import json
@@ -47,24 +50,37 @@ def _cpu_worker(args):
     return steps, time.perf_counter() - t0
 
 
-def cpu_baseline(name, workers, steps):
+def _pool_run(name, workers, steps):
     ctx = mp.get_context("fork")  # before any GPU initialisation in this process
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
         res = pool.map(_cpu_worker, [(name, steps, 1000 + i) for i in range(workers)])
     wall = time.perf_counter() - t0
-    total = sum(r[0] for r in res)
+    return sum(r[0] for r in res) / wall, sum(r[0] / r[1] for r in res) / workers, wall
+
+
+def cpu_baseline(name, workers, steps):
+    """The C oracle restatement (1 env per process, resets included) on 1 core and on `workers`
+    cores of this host.  On the GPU box `workers` is the job's CPU share (16 of the host's CPUs);
+    the whole-host figure is the per-core rate times the host's CPU count, labelled as scaled."""
+    one, _, wall1 = _pool_run(name, 1, 2 * steps)
+    many, per_core, wall = _pool_run(name, workers, steps)
     cpu_model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
             cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), cpu_model)
     except OSError:
         pass
-    return {"value": round(total / wall, 1), "unit": "env-steps/s", "cores": workers, "kind": "port",
-            "cpu_model": cpu_model, "host_cpus": os.cpu_count(),
-            "sample": f"{workers} processes x 1 env x {steps} steps of {name} (C oracle restatement, "
-                      f"1 env per core, incl. resets); wall {wall:.1f}s",
-            "per_core_env_steps_s": round(sum(r[0] / r[1] for r in res) / workers, 1)}
+    host = os.cpu_count() or workers
+    return {"value": round(many, 1), "unit": "env-steps/s", "cores": workers, "kind": "port",
+            "cpu_model": cpu_model, "host_cpus": host,
+            "sample": f"C oracle restatement of {name}, 1 env per process incl. resets: 1 process x {2 * steps} "
+                      f"steps (wall {wall1:.1f}s), then {workers} processes x {steps} steps (wall {wall:.1f}s)",
+            "one_core_env_steps_s": round(one, 1),
+            "per_core_env_steps_s": round(per_core, 1),
+            "host_scaled_env_steps_s": round(per_core * host, 1),
+            "host_scaled_note": f"per-core rate x {host} host CPUs (linear scaling assumed, not measured: "
+                                f"the job may use {workers} of them)"}
 
 
 def load_pmc(kernel, workload, envs):
@@ -91,6 +107,8 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--cpu-steps", type=int, default=1500)  # ~16 x 1 s of CPU work (about 15-25 s)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-phase-spread", action="store_true",
+                    help="start every env at episode step 0 (resets then happen on the same step for all envs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,6 +136,10 @@ def main():
     lib = vec.lib
     actions = torch.empty(n, dtype=torch.uint8, device=device)
     vec.reset()
+    phase_spread = not args.no_phase_spread and spec.max_episode_steps > 1
+    if phase_spread:  # env i starts at episode step (global id) mod max_episode_steps
+        L = spec.max_episode_steps
+        vec.set_episode_steps(torch.tensor([(rank * n + i) % L for i in range(n)], dtype=torch.int32))
     for s in range(args.warmup):
         vec.random_actions(s, out=actions)
         vec.step(actions)
@@ -135,9 +157,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     import ctypes
-    tm = (ctypes.c_double * 3)()
+    tm = (ctypes.c_double * 4)()
     native.check(lib.mg_read_timing(vec.handle, tm))
     t_step_ms, t_render_ms, n_timed = tm[0] / args.steps, tm[1] / args.steps, int(tm[2])
+    t_reset_ms = tm[3] / args.steps
     errors = int((vec.errors() != 0).sum().item())
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -168,13 +191,14 @@ def main():
             "data": "synthetic (device Philox uniform actions over the 18 discrete actions; env i seeded 1000+i)",
             "config": {"workload": args.env, "envs_per_gpu": n, "episode_steps": spec.max_episode_steps,
                        "physics_substeps": 10, "solver_iterations": 10, "render": "2 x 384^2 -> 96^2",
+                       "phase_spread": phase_spread,
                        "parallelism": f"dp{world} (envs sharded, no data-path collective)"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": pmc, "bytes_per_env_step": per_env, "units_per_launch": n,
                          "kernel_avg_ms": round(dom_ms, 4)},
-            "kernel_ms_per_step": {"step_kernel": round(t_step_ms, 4), "render_kernel": round(t_render_ms, 4),
-                                   "timed_launches": n_timed},
+            "kernel_ms_per_step": {"step_kernel": round(t_step_ms, 4), "reset_kernel": round(t_reset_ms, 4),
+                                   "render_kernel": round(t_render_ms, 4), "timed_launches": n_timed},
             "env_errors": errors,
             "cpu_baseline": cpu,
         }

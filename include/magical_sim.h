@@ -90,8 +90,11 @@ int mg_selftest_sincos(const double *x_dev, double *sin_dev, double *cos_dev, in
 /* per-kernel timing of the next max_steps mg_step calls (hipEvents on the launch stream); 0 disables */
 int mg_enable_timing(mg_sim *sim, int max_steps);
 /* out[0] = total ms in the physics/step kernel, out[1] = total ms in the render kernel,
- * out[2] = number of mg_step calls timed; resets the counters */
+ * out[2] = number of mg_step calls timed, out[3] = total ms in the auto-reset kernel; resets the counters */
 int mg_read_timing(mg_sim *sim, double *out);
+/* overwrite every env's episode step counter (BaseEnv.episode_steps, base_env.py:279-283) from device
+ * i32[N]: throughput runs stagger episode phases so resets are spread over the timed steps */
+int mg_set_episode_steps(mg_sim *sim, const int32_t *steps_dev, void *stream);
 void mg_destroy(mg_sim *sim);
 const char *mg_last_error(void);
 

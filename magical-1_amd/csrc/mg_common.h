@@ -47,6 +47,10 @@ enum { MG_XF_MAIN = 0, MG_XF_FINGER_L = 1, MG_XF_FINGER_R = 2, MG_XF_PUPIL_L = 3
        MG_XF_STATIC0 = 8 };
 enum { MG_OUTLINE_NONE = 0, MG_OUTLINE_SOLID = 1, MG_OUTLINE_DASHED = 2 };
 
+// shape filter: a shape whose categories were left 0 by pm_randomise_all_poses (geom.py:300-319, after a
+// failed layout retry) collides with nothing; reset_env folds that into its group as this bit
+#define MG_GROUP_OFF 0x4000
+
 // constraint kinds
 enum { MG_C_PIVOT = 0, MG_C_GEAR = 1, MG_C_ROTLIMIT = 2, MG_C_MOTOR = 3, MG_C_SPRING = 4 };
 

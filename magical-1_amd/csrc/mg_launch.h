@@ -26,6 +26,21 @@ size_t mg_step_lds_bytes(const StepCaps &c, int blk);
 int mg_step_variant(const StepCaps &c, int n_envs);
 // compiled envs-per-workgroup sizes of a variant
 bool mg_step_blk_ok(int variant, int blk);
+// Slot caps of the LDS-resident variants (compile-time, so every LDS address folds to a constant
+// offset from the lane's column): 0 = state stays in HBM.
+__host__ __device__ constexpr StepCaps step_variant_caps(int v) {
+    return v == 1 ? StepCaps{6, 5, 10, 20, 16}    // robot only (MoveToRegion)
+         : v == 2 ? StepCaps{7, 6, 12, 32, 16}    // robot + one single-shape block (MoveToCorner)
+         : v == 3 ? StepCaps{14, 53, 26, 48, 1}   // up to 8 blocks incl. stars (Cluster*, MatchRegions): runtime lists
+         : v == 4 ? StepCaps{14, 53, 26, 48, 1}   // the same scenes, one env per 64-lane wavefront (cooperative)
+         : StepCaps{0, 0, 0, 0, 0};
+}
+
+// one compiled step-kernel form (defined in mg_stepk.h, instantiated in mg_step_*.hip)
+template <int VAR, int BLK>
+hipError_t launch_step_var(const MGState &S, const mg_library *L, TaskCfg cfg, int max_steps, int auto_reset,
+                           const uint8_t *actions, float *reward, uint8_t *done, double *eval_score,
+                           uint8_t *reset_mask, hipStream_t st);
 hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, int variant, int blk, int max_steps,
                           int auto_reset, const uint8_t *actions, float *reward, uint8_t *done, double *eval_score,
                           uint8_t *reset_mask, hipStream_t st);
@@ -34,4 +49,9 @@ hipError_t mg_launch_compose3ea(const MGState &S, const uint8_t *obs_allo, const
                                 hipStream_t st);
 // profiling builds (-DMG_PROFILE): copy and clear each translation unit's phase timers
 hipError_t mg_prof_read_physics(unsigned long long *out64);
+hipError_t mg_prof_read_reset(unsigned long long *out64);
+hipError_t mg_prof_read_step_robot(unsigned long long *out64);
+hipError_t mg_prof_read_step_v3(unsigned long long *out64);
+hipError_t mg_prof_read_step_v4(unsigned long long *out64);
+hipError_t mg_prof_read_step_hbm(unsigned long long *out64);
 hipError_t mg_prof_read_raster(unsigned long long *out64);

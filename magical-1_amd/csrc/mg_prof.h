@@ -3,7 +3,7 @@
 // them to g_prof at the end; the production build compiles these to nothing.
 #pragma once
 #ifdef MG_PROFILE
-__device__ unsigned long long g_prof[64];
+static __device__ unsigned long long g_prof[64]; // one per translation unit
 #define MG_PROF_BEGIN(on) const bool _pon = (on); unsigned long long _pt = __builtin_amdgcn_s_memtime(); \
     unsigned long long _pacc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define MG_PROF(i) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); _pacc[i] += _t - _pt; _pt = _t; } while (0)
@@ -18,6 +18,21 @@ __device__ unsigned long long g_prof[64];
 #define MG_PROF_BEGIN(on)
 #define MG_PROF(i) do { } while (0)
 #define MG_PROF_END(base) do { } while (0)
+#endif
+
+// host reader of this translation unit's timers: adds them to out[64] and clears them
+#ifdef MG_PROFILE
+#define MG_PROF_READER(fn)                                                                     \
+    hipError_t fn(unsigned long long *out) {                                                   \
+        unsigned long long v[64], z[64] = {0};                                                 \
+        hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_prof), sizeof(v));                  \
+        if (e != hipSuccess) return e;                                                         \
+        for (int i = 0; i < 64; i++) out[i] += v[i];                                           \
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z));                            \
+    }
+#else
+#define MG_PROF_READER(fn) \
+    hipError_t fn(unsigned long long *out) { (void)out; return hipSuccess; }
 #endif
 
 // phase timers threaded through device functions

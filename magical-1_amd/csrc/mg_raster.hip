@@ -52,15 +52,4 @@ hipError_t mg_launch_compose3ea(const MGState &S, const uint8_t *obs_allo, const
     return hipGetLastError();
 }
 
-hipError_t mg_prof_read_raster(unsigned long long *out) {
-#ifdef MG_PROFILE
-    unsigned long long v[64], z[64] = {0};
-    hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_prof), sizeof(v));
-    if (e != hipSuccess) return e;
-    for (int i = 0; i < 64; i++) out[i] += v[i];
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z));
-#else
-    (void)out;
-    return hipSuccess;
-#endif
-}
+MG_PROF_READER(mg_prof_read_raster)

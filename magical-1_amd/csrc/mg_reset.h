@@ -170,7 +170,8 @@ MG_DEV void add_block(const MGState &S, const mg_library *L, int e, Builder &B, 
 // A is entity self_ent's shape (or goal); ign = bit mask of entities whose shapes are ignored
 // (pm_randomise_pose ignore_shapes, geom.py:116-264).
 MG_DEV bool query_hits(const MGState &S, const mg_library *L, int e, const ShapeW &A, int self_k, int group, int self_ent,
-                       uint32_t ign) {
+                       uint32_t ign, bool self_on) {
+    if (!self_on) return false; // the queried shape's categories are 0: cpShapeFilterReject for every pair
     for (int w = 0; w < 4; w++) {
         ShapeW W;
         load_wall(w, W);
@@ -204,6 +205,9 @@ MG_DEV bool query_hits(const MGState &S, const mg_library *L, int e, const Shape
     return false;
 }
 
+MG_DEV int ent_enabled(const MGState &S, int e, int ent) {
+    return AT(S.ekind, ent) == MG_ENT_GOAL ? AT(S.eshape0, ent) : AT(S.scat, AT(S.eshape0, ent));
+}
 MG_DEV void ent_set_enabled(const MGState &S, int e, int ent, int on) {
     if (AT(S.ekind, ent) == MG_ENT_GOAL) { AT(S.eshape0, ent) = (int8_t)on; return; }
     int s0 = AT(S.eshape0, ent), n = AT(S.enshapes, ent);
@@ -240,13 +244,13 @@ MG_DEV bool entity_collides(const MGState &S, const mg_library *L, int e, int en
     if (AT(S.ekind, ent) == MG_ENT_GOAL) {
         ShapeW G;
         load_goal(AT(S.ex, ent), AT(S.ey, ent), AT(S.ew, ent), AT(S.eh, ent), 0, G);
-        return query_hits(S, L, e, G, -1, 0, ent, ign);
+        return query_hits(S, L, e, G, -1, 0, ent, ign, AT(S.eshape0, ent) != 0);
     }
     int s0 = AT(S.eshape0, ent), n = AT(S.enshapes, ent);
     for (int k = s0; k < s0 + n; k++) {
         ShapeW A;
         load_shape(S, L, e, k, 0, A);
-        if (query_hits(S, L, e, A, k, AT(S.sgroup, k), ent, ign)) return true;
+        if (query_hits(S, L, e, A, k, AT(S.sgroup, k), ent, ign, AT(S.scat, k) != 0)) return true;
     }
     return false;
 }
@@ -265,24 +269,52 @@ MG_DEV int randomise_pose(const MGState &S, const mg_library *L, int e, int ent,
     }
     double rmin = -3.141592653589793, rmax = 3.141592653589793;
     if (rot_limit >= 0) { rmin = orig_a - rot_limit; rmax = orig_a + rot_limit; }
-    for (int tries = 0; tries < 10000; tries++) {
+    double saved_x[6], saved_y[6], saved_a[6]; // geom.py:174-176 saved_positions / saved_angles
+    if (!goal) {
+        const int nb = AT(S.ekind, ent) == MG_ENT_ROBOT ? 6 : 1;
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const int b = b0 + (k < nb ? k : 0);
+            saved_x[k] = AT(S.bpx, b); saved_y[k] = AT(S.bpy, b); saved_a[k] = AT(S.ba, b);
+        }
+    }
+    for (int tries = 0; tries < S.max_tries; tries++) {
         double x = mt_uniform(S, e, xlo, xhi);
         double y = mt_uniform(S, e, ylo, yhi);
         double a = rand_rot ? mt_uniform(S, e, rmin, rmax) : orig_a;
         shift_entity(S, e, ent, v2(x, y), a);
         if (!entity_collides(S, L, e, ent, ign)) return 0;
     }
-    shift_entity(S, e, ent, orig_p, orig_a);
+    // PlacementError: every body back to its saved absolute pose (geom.py:250-254: Body.position and
+    // Body.angle setters), not a rigid shift relative to the last try
+    if (goal) {
+        AT(S.ex, ent) = orig_p.x; AT(S.ey, ent) = orig_p.y;
+    } else {
+        const int nb = AT(S.ekind, ent) == MG_ENT_ROBOT ? 6 : 1;
+        for (int k = 0; k < nb; k++) {
+            const int b = b0 + k;
+            body_set_angle(S, e, b, saved_a[k]);
+            const double c = AT(S.brc, b), sn = AT(S.brs, b);
+            AT(S.bpx, b) = (c * 0.0 + (-sn) * 0.0) + saved_x[k]; // cpBodySetPosition: p = T(cog = 0) + position
+            AT(S.bpy, b) = (sn * 0.0 + c * 0.0) + saved_y[k];
+        }
+    }
     return -1;
 }
 
 MG_DEV void randomise_all(const MGState &S, const mg_library *L, int e, const int *ents, int n, const bool *rand_rot,
                           double pos_limit, const double *rot_limits, uint32_t ign = 0u) {
     for (int retry = 0; retry < 10; retry++) {
-        for (int k = 0; k < n; k++) ent_set_enabled(S, e, ents[k], 0);
+        // geom.py:300-319: each entity's filter is captured at the start of every retry and restored when
+        // its turn comes, so entities left disabled by a failed retry stay disabled (categories 0)
+        uint32_t saved = 0u;
+        for (int k = 0; k < n; k++) {
+            saved |= (uint32_t)(ent_enabled(S, e, ents[k]) != 0) << k;
+            ent_set_enabled(S, e, ents[k], 0);
+        }
         bool failed = false;
         for (int k = 0; k < n && !failed; k++) {
-            ent_set_enabled(S, e, ents[k], 1);
+            ent_set_enabled(S, e, ents[k], (saved >> k) & 1u);
             if (randomise_pose(S, L, e, ents[k], rand_rot[k], pos_limit, rot_limits[k], ign) != 0) failed = true;
         }
         if (!failed) return;
@@ -652,5 +684,8 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
         }
     }
     S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
-    for (int k = 0; k < B.ns; k++) AT(S.scat, k) = 1;
+    // shapes left with categories 0 by the randomiser collide with nothing for the episode (step broadphase,
+    // goal queries): folded into the group the step kernels already read
+    for (int k = 0; k < B.ns; k++)
+        if (!AT(S.scat, k)) AT(S.sgroup, k) = (int16_t)(AT(S.sgroup, k) | MG_GROUP_OFF);
 }

@@ -1,0 +1,30 @@
+// mg_reset.hip -- seed (MT19937 per env) and reset (BaseEnv.reset + on_reset, masked) kernels.
+#include "mg_launch.h"
+#include "mg_reset.h"
+__global__ void __launch_bounds__(64) seed_kernel(MGState S, const uint32_t *__restrict__ seeds) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= S.n_envs) return;
+    mt_seed(S, e, seeds[e]);
+}
+
+__global__ void __launch_bounds__(64) reset_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg,
+                                                   const uint8_t *__restrict__ mask) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= S.n_envs) return;
+    if (mask && !mask[e]) return;
+    reset_env(S, L, e, cfg);
+}
+
+static int grid64(const MGState &S) { return (S.n_envs + 63) / 64; }
+
+hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream_t st) {
+    hipLaunchKernelGGL(seed_kernel, dim3(grid64(S)), dim3(64), 0, st, S, seeds_dev);
+    return hipGetLastError();
+}
+
+hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, const uint8_t *mask, hipStream_t st) {
+    hipLaunchKernelGGL(reset_kernel, dim3(grid64(S)), dim3(64), 0, st, S, L, cfg, mask);
+    return hipGetLastError();
+}
+
+MG_PROF_READER(mg_prof_read_reset)

@@ -65,6 +65,7 @@ MG_DEV int longest_line(const double *px, const double *py, int n, double inlier
 // entities.py:803-863 get_overlapping_ents(com_overlap=True) of goal entity ge over the blocks: bit i set
 // when every shape of block i overlaps the goal with its body's position inside the goal's BB
 MG_DEV uint32_t goal_overlap_blocks(const MGState &S, const mg_library *L, int e, int ge) {
+    if (AT(S.eshape0, ge) == 0) return 0u; // the goal's categories are 0 (MG_GROUP_OFF): the query rejects all
     ShapeW G;
     load_goal(AT(S.ex, ge), AT(S.ey, ge), AT(S.ew, ge), AT(S.eh, ge), 0, G);
     const int nents = S.nents[e];
@@ -77,7 +78,7 @@ MG_DEV uint32_t goal_overlap_blocks(const MGState &S, const mg_library *L, int e
             ShapeW A;
             load_shape(S, L, e, k, 0, A);
             bool hit = false;
-            if (bb_intersects(G, A)) {
+            if (bb_intersects(G, A) && !(AT(S.sgroup, k) & MG_GROUP_OFF)) {
                 Collision info;
                 collide(G, A, info);
                 if (info.count) {

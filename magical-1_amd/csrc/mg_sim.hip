@@ -41,7 +41,7 @@ struct mg_sim {
     uint8_t *reset_mask; // device u8[N]: envs to auto-reset after the step
     // optional per-kernel timing (hipEvents on the launch stream)
     int timing;
-    std::vector<hipEvent_t> ev;   // triples: before step_kernel, between kernels, after render_kernel
+    std::vector<hipEvent_t> ev;   // quadruples: before step_kernel, after it, after the auto-reset, after render_kernel
     size_t ev_used;
 };
 
@@ -259,6 +259,8 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     s->S.n_envs = cfg->num_envs;
     s->S.cons_cap = MG_MAX_CONS;
     s->S.arb_cap = MG_MAX_ARB;
+    s->S.max_tries = 10000; // geom.py:198
+    if (const char *mt = getenv("MG_DEBUG_MAX_TRIES")) s->S.max_tries = atoi(mt) > 0 ? atoi(mt) : 10000; // tests only
     s->S.N = (cfg->num_envs + 63) / 64 * 64;
     Carver sizing = {nullptr, 0};
     layout(s->S, sizing);
@@ -331,15 +333,16 @@ int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
     hipStream_t st = as_stream(stream);
     TaskCfg cfg = {s->task, s->flags};
     hipEvent_t *ev = nullptr;
-    if (s->timing && s->ev_used + 3 <= s->ev.size()) { ev = &s->ev[s->ev_used]; s->ev_used += 3; }
+    if (s->timing && s->ev_used + 4 <= s->ev.size()) { ev = &s->ev[s->ev_used]; s->ev_used += 4; }
     if (ev) HIPC(hipEventRecord(ev[0], st));
     HIPC(mg_launch_step(s->S, s->dlib, cfg, s->step_variant, s->step_blk, s->max_steps, s->auto_reset, actions, s->out.reward,
                         s->out.done, s->out.eval_score, s->reset_mask, st));
-    if (s->auto_reset) HIPC(mg_launch_reset(s->S, s->dlib, cfg, s->reset_mask, st));
     if (ev) HIPC(hipEventRecord(ev[1], st));
+    if (s->auto_reset) HIPC(mg_launch_reset(s->S, s->dlib, cfg, s->reset_mask, st));
+    if (ev) HIPC(hipEventRecord(ev[2], st));
     int rc = 0;
     if (s->preproc != MG_PREPROC_NONE) rc = render_lores(s, st, nullptr);
-    if (ev) HIPC(hipEventRecord(ev[2], st));
+    if (ev) HIPC(hipEventRecord(ev[3], st));
     return rc;
 }
 
@@ -407,6 +410,19 @@ int mg_random_actions(mg_sim *s, uint8_t *actions, uint64_t key, uint64_t step, 
 
 int mg_num_envs(const mg_sim *s) { return s ? s->S.n_envs : -22; }
 
+__global__ void __launch_bounds__(64) set_episode_steps_kernel(MGState S, const int32_t *steps) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < S.n_envs) S.episode_steps[e] = steps[e];
+}
+
+int mg_set_episode_steps(mg_sim *s, const int32_t *steps, void *stream) {
+    if (!s || !steps) return set_err(-22, "mg_set_episode_steps: null argument");
+    HIPC(hipSetDevice(s->device));
+    hipLaunchKernelGGL(set_episode_steps_kernel, dim3(grid64(s)), dim3(64), 0, as_stream(stream), s->S, steps);
+    HIPC(hipGetLastError());
+    return 0;
+}
+
 int mg_enable_timing(mg_sim *s, int max_steps) {
     if (!s) return set_err(-22, "mg_enable_timing: null sim");
     HIPC(hipSetDevice(s->device));
@@ -414,7 +430,7 @@ int mg_enable_timing(mg_sim *s, int max_steps) {
     s->ev.clear();
     s->ev_used = 0;
     s->timing = max_steps > 0;
-    for (int i = 0; i < 3 * max_steps; i++) {
+    for (int i = 0; i < 4 * max_steps; i++) {
         hipEvent_t e;
         HIPC(hipEventCreate(&e));
         s->ev.push_back(e);
@@ -424,16 +440,18 @@ int mg_enable_timing(mg_sim *s, int max_steps) {
 
 int mg_read_timing(mg_sim *s, double *out) {
     if (!s || !out) return set_err(-22, "mg_read_timing: null argument");
-    double t_step = 0.0, t_render = 0.0;
-    int n = (int)(s->ev_used / 3);
+    double t_step = 0.0, t_render = 0.0, t_reset = 0.0;
+    int n = (int)(s->ev_used / 4);
     for (int i = 0; i < n; i++) {
-        float a = 0.f, b = 0.f;
-        HIPC(hipEventSynchronize(s->ev[3 * i + 2]));
-        HIPC(hipEventElapsedTime(&a, s->ev[3 * i], s->ev[3 * i + 1]));
-        HIPC(hipEventElapsedTime(&b, s->ev[3 * i + 1], s->ev[3 * i + 2]));
-        t_step += a; t_render += b;
+        float a = 0.f, b = 0.f, c = 0.f;
+        const hipEvent_t *ev = &s->ev[4 * i];
+        HIPC(hipEventSynchronize(ev[3]));
+        HIPC(hipEventElapsedTime(&a, ev[0], ev[1]));
+        HIPC(hipEventElapsedTime(&c, ev[1], ev[2]));
+        HIPC(hipEventElapsedTime(&b, ev[2], ev[3]));
+        t_step += a; t_render += b; t_reset += c;
     }
-    out[0] = t_step; out[1] = t_render; out[2] = n;
+    out[0] = t_step; out[1] = t_render; out[2] = n; out[3] = t_reset;
     s->ev_used = 0;
     return 0;
 }

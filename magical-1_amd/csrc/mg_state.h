@@ -13,6 +13,7 @@ struct MGState {
     int N;      // padded env count (multiple of 64); row stride of every [slot][N] array
     int n_envs; // live env count
     int cons_cap, arb_cap; // constraint / arbiter slots per env (MG_MAX_* in HBM; smaller in LDS views)
+    int max_tries;         // pm_randomise_pose max_tries (geom.py:198: 10000; tests lower it to force layout retries)
     // ---- bodies [MG_MAX_BODIES][N] ----
     double *bpx, *bpy, *bvx, *bvy, *ba, *bw, *bvbx, *bvby, *bwb, *brc, *brs, *bminv, *biinv, *bacache;
     int8_t *bkin;   // 1 = kinematic

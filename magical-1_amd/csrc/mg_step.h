@@ -670,7 +670,7 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
         bool have_a = false;
         const int gi = AT(S.sgroup, i), bi = AT(S.sbody, i);
         const double ui = AT(S.su, i);
-        for (int w = 0; w < 4; w++) {
+        for (int w = 0; w < 4 && !(gi & MG_GROUP_OFF); w++) { // categories 0 collide with nothing
             double wl, wb, wr, wt;
             wall_bb(w, wl, wb, wr, wt);
             if (!(al <= wr && wl <= ar && ab <= wt && wb <= at)) continue;
@@ -686,7 +686,7 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
                 continue;
             if (AT(S.sbody, j) == bi) continue;
             int gj = AT(S.sgroup, j);
-            if (gi != 0 && gi == gj) continue;
+            if ((gi != 0 && gi == gj) || ((gi | gj) & MG_GROUP_OFF)) continue; // cpShapeFilterReject
             if (!have_a) { load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A); have_a = true; }
             ShapeW B;
             load_shape(S, L, e, j, (uint64_t)AT(S.shash, j), B);
@@ -1035,7 +1035,7 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
                 j = -1 - r;
                 double wl, wb, wr, wt;
                 wall_bb(r, wl, wb, wr, wt);
-                if (al <= wr && wl <= ar && ab <= wt && wb <= at) {
+                if (al <= wr && wl <= ar && ab <= wt && wb <= at && !(AT(S.sgroup, i) & MG_GROUP_OFF)) {
                     ShapeW A, W;
                     load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A);
                     load_wall(r, W);
@@ -1045,7 +1045,7 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
                 j = i + 1 + (r - 4);
                 const int gi = AT(S.sgroup, i), gj = AT(S.sgroup, j);
                 if (al <= AT(S.sbbr, j) && AT(S.sbbl, j) <= ar && ab <= AT(S.sbbt, j) && AT(S.sbbb, j) <= at &&
-                    AT(S.sbody, j) != AT(S.sbody, i) && !(gi != 0 && gi == gj)) {
+                    AT(S.sbody, j) != AT(S.sbody, i) && !(gi != 0 && gi == gj) && !((gi | gj) & MG_GROUP_OFF)) {
                     ShapeW A, B;
                     load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A);
                     load_shape(S, L, e, j, (uint64_t)AT(S.shash, j), B);

@@ -1,0 +1,238 @@
+// mg_stepk.h -- the step kernel template (action decode, 10 x [Robot.update + cpSpaceStep], episode
+// counter, score) and its launcher.  Each form is instantiated in its own translation unit
+// (mg_step_robot.hip, mg_step_v3.hip, mg_step_v4.hip, mg_step_hbm.hip) so they compile in parallel;
+// mg_physics.hip dispatches.
+#pragma once
+#include "mg_launch.h"
+#include "mg_score.h"
+
+// ---- LDS-resident substeps ------------------------------------------------
+// The 10 substeps of an env-step touch only the env's bodies, shapes,
+// constraints, arbiters and a few scalars.  They are copied once per env-step
+// from HBM ([slot][N] arrays) into LDS ([slot][BLK] arrays, one column per lane)
+// and the MGState "view" V points there with V.N = BLK and e = lane, so the same
+// device code runs against LDS; everything is copied back before scoring and
+// the in-place reset (which use the HBM state).  A lane only touches its own
+// column, so no barrier is needed.
+template <typename T>
+__device__ __forceinline__ T *carve(unsigned char *base, size_t &off, size_t count) {
+    off = (off + 15) & ~(size_t)15;
+    T *p = (T *)(base + off);
+    off += count * sizeof(T);
+    return p;
+}
+
+__device__ __forceinline__ void carve_view(MGState &V, unsigned char *smem, const StepCaps &c, int blk) {
+    size_t off = 0;
+    const size_t B = (size_t)c.nb * blk, SH = (size_t)c.ns * blk, C = (size_t)c.nc * blk, A = (size_t)c.na * blk;
+    V.bpx = carve<double>(smem, off, B); V.bpy = carve<double>(smem, off, B); V.bvx = carve<double>(smem, off, B);
+    V.bvy = carve<double>(smem, off, B); V.ba = carve<double>(smem, off, B); V.bw = carve<double>(smem, off, B);
+    V.bvbx = carve<double>(smem, off, B); V.bvby = carve<double>(smem, off, B); V.bwb = carve<double>(smem, off, B);
+    V.brc = carve<double>(smem, off, B); V.brs = carve<double>(smem, off, B); V.bminv = carve<double>(smem, off, B);
+    V.biinv = carve<double>(smem, off, B); V.bacache = carve<double>(smem, off, B);
+    V.sr = carve<double>(smem, off, SH); V.su = carve<double>(smem, off, SH); V.sbbl = carve<double>(smem, off, SH);
+    V.sbbb = carve<double>(smem, off, SH); V.sbbr = carve<double>(smem, off, SH); V.sbbt = carve<double>(smem, off, SH);
+    V.cp = carve<double>(smem, off, (size_t)CP_NUM * C);
+    V.anx = carve<double>(smem, off, A); V.any = carve<double>(smem, off, A); V.au = carve<double>(smem, off, A);
+    V.acon = carve<double>(smem, off, (size_t)2 * AC_NUM * A); V.ahash = carve<uint64_t>(smem, off, 2 * A);
+    V.curr_dt = carve<double>(smem, off, blk); V.target_speed = carve<double>(smem, off, blk);
+    V.rel_turn = carve<double>(smem, off, blk); V.target_finger = carve<double>(smem, off, blk);
+    V.akey = carve<int32_t>(smem, off, A); V.astamp = carve<uint32_t>(smem, off, A);
+    V.nbodies = carve<int32_t>(smem, off, blk); V.nshapes = carve<int32_t>(smem, off, blk);
+    V.ncons = carve<int32_t>(smem, off, blk); V.nactive = carve<int32_t>(smem, off, blk);
+    V.stamp = carve<uint32_t>(smem, off, blk); V.overflow = carve<int32_t>(smem, off, blk);
+    V.robot_body0 = carve<int32_t>(smem, off, blk); V.robot_cons0 = carve<int32_t>(smem, off, blk);
+    V.sgroup = carve<int16_t>(smem, off, SH); V.shash = carve<int16_t>(smem, off, SH);
+    V.sbody = carve<int8_t>(smem, off, SH); V.spoly = carve<int8_t>(smem, off, SH);
+    V.ctype = carve<int8_t>(smem, off, C); V.ca = carve<int8_t>(smem, off, C); V.cb = carve<int8_t>(smem, off, C);
+    V.astate = carve<int8_t>(smem, off, A); V.acount = carve<int8_t>(smem, off, A); V.asa = carve<int8_t>(smem, off, A);
+    V.asb = carve<int8_t>(smem, off, A); V.active = carve<int8_t>(smem, off, A);
+    V.N = blk;
+    V.cons_cap = c.nc;
+    V.arb_cap = c.na;
+}
+
+// rows [0, rows) of a [row][N] HBM array <-> [row][BLK] LDS array (lane's column); for the
+// cp / acon / ahash blocks the HBM row of LDS row (k, r) is k * hcap + r
+template <typename T>
+__device__ __forceinline__ void xfer(T *lds, T *hbm, int rows, int blk, int lane, int N, int e, bool to_lds,
+                                     int r0 = 0, int rs = 1, int groups = 1, int lcap = 0, int hcap = 0) {
+#pragma unroll 1
+    for (int g = 0; g < groups; g++)
+#pragma unroll 2
+        for (int r = r0; r < rows; r += rs) {
+            const uint32_t li = (uint32_t)(g * lcap + r) * blk + lane, hi = (uint32_t)(g * hcap + r) * N + e;
+            if (to_lds) lds[li] = hbm[hi]; else hbm[hi] = lds[li];
+        }
+}
+
+// HBM <-> LDS view transfer of what the substeps read (in) / what later env-steps need (out):
+// bodies (incl. bias velocities and the rotation cache), the constraints' parameters and
+// warm-start impulses, the live arbiters (key, contacts, warm-start hashes) and the active list.
+// Cached shape BBs and the constraints' pre-step products are recomputed before use.
+// (r0, rs): rows r0, r0 + rs, ... of every array (rs = 64, r0 = lane: the cooperative form, one env per
+// wavefront, each lane a share of the rows)
+__device__ __forceinline__ void xfer_state(const MGState &S, const MGState &V, const StepCaps &c, int lane, int e,
+                                           bool in, bool cons_list = false, int r0 = 0, int rs = 1) {
+    const int blk = V.N, N = S.N;
+#define XF(f, rows) xfer(V.f, S.f, rows, blk, lane, N, e, in, r0, rs)
+#define XS(f, r) do { if (in) V.f[(uint32_t)(r) * blk + lane] = S.f[(uint32_t)(r) * N + e]; \
+                      else S.f[(uint32_t)(r) * N + e] = V.f[(uint32_t)(r) * blk + lane]; } while (0)
+    XF(bpx, c.nb); XF(bpy, c.nb); XF(bvx, c.nb); XF(bvy, c.nb); XF(ba, c.nb); XF(bw, c.nb); XF(bvbx, c.nb);
+    XF(bvby, c.nb); XF(bwb, c.nb); XF(brc, c.nb); XF(brs, c.nb); XF(bacache, c.nb);
+    // constraint parameter slots: in = MAXF, MAXB, BCOEF, JACC, JACC2, type parameters 8-11; out = JACC, JACC2
+#pragma unroll 1
+    for (int k = 0; k < CP_NUM; k++) {
+        const bool need = in ? (k <= CP_JACC2 || (k >= 8 && k <= 11)) : (k == CP_JACC || k == CP_JACC2);
+        if (!need) continue;
+#pragma unroll 2
+        for (int r = r0; r < c.nc; r += rs) {
+            const uint32_t li = (uint32_t)(k * c.nc + r) * blk + lane, hi = (uint32_t)(k * MG_MAX_CONS + r) * N + e;
+            if (in) V.cp[li] = S.cp[hi]; else S.cp[hi] = V.cp[li];
+        }
+    }
+#pragma unroll 1
+    for (int r = r0; r < c.na; r += rs) { // arbiter slots: only live ones carry data
+        XS(akey, r);
+        const int key = in ? V.akey[(uint32_t)r * blk + lane] : V.akey[(uint32_t)r * blk + lane];
+        if (key < 0) continue;
+        XS(anx, r); XS(any, r); XS(au, r); XS(astamp, r); XS(astate, r); XS(acount, r); XS(asa, r); XS(asb, r);
+#pragma unroll 1
+        for (int f = 0; f < 2 * AC_NUM; f++) {
+            if (in) V.acon[(uint32_t)(f * c.na + r) * blk + lane] = S.acon[(uint32_t)(f * MG_MAX_ARB + r) * N + e];
+            else S.acon[(uint32_t)(f * MG_MAX_ARB + r) * N + e] = V.acon[(uint32_t)(f * c.na + r) * blk + lane];
+        }
+        for (int k = 0; k < 2; k++) {
+            if (in) V.ahash[(uint32_t)(k * c.na + r) * blk + lane] = S.ahash[(uint32_t)(k * MG_MAX_ARB + r) * N + e];
+            else S.ahash[(uint32_t)(k * MG_MAX_ARB + r) * N + e] = V.ahash[(uint32_t)(k * c.na + r) * blk + lane];
+        }
+    }
+    XF(nactive, 1);
+    const int nact = in ? S.nactive[e] : V.nactive[lane];
+#pragma unroll 1
+    for (int r = r0; r < nact; r += rs) XS(active, r);
+    XF(curr_dt, 1); XF(stamp, 1); XF(overflow, 1);
+    if (in) { // read-only during the substeps
+        XF(target_speed, 1); XF(rel_turn, 1); XF(target_finger, 1);
+        XF(bminv, c.nb); XF(biinv, c.nb);
+        XF(sr, c.ns); XF(su, c.ns); XF(sgroup, c.ns); XF(shash, c.ns); XF(sbody, c.ns); XF(spoly, c.ns);
+        XF(nbodies, 1); XF(nshapes, 1); XF(ncons, 1); XF(robot_body0, 1); XF(robot_cons0, 1);
+        if (cons_list) { XF(ctype, c.nc); XF(ca, c.nc); XF(cb, c.nc); } // runtime constraint list
+    }
+#undef XS
+#undef XF
+}
+
+// Workgroups are dispatched round-robin over the 8 XCDs (workgroup b -> XCD b % 8); map them so
+// that each XCD owns one contiguous range of envs: neighbouring envs share [slot][N] cache lines,
+// and with few envs per workgroup those lines are then reused in the XCD's own L2.
+__device__ __forceinline__ int xcd_block(int b, int g) {
+    const int q = g >> 3, r = g & 7, x = b & 7;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+
+// Robot.set_action + 10 x (Robot.update, cpSpaceStep): base_env.py:248-276
+template <int NCS>
+__device__ __forceinline__ void env_substeps(const MGState &V, const mg_library *L, int ev, int a, MGProf &P) {
+    robot_set_action(V, L, ev, a < 18 ? a : 0);
+    const double dt = L->dt;
+    for (int i = 0; i < 10; i++) {
+        robot_update(V, L, ev);
+        MG_PP(P, 0);
+        space_step<NCS>(V, L, ev, dt, P);
+    }
+}
+
+// the same with one env per wavefront: lane 0 drives the robot, every lane takes part in the step
+__device__ __forceinline__ void env_substeps_coop(const MGState &V, const mg_library *L, int lane, int a, MGProf &P) {
+    if (lane == 0) robot_set_action(V, L, 0, a < 18 ? a : 0);
+    const double dt = L->dt;
+    for (int i = 0; i < 10; i++) {
+        __syncthreads();
+        if (lane == 0) robot_update(V, L, 0);
+        __syncthreads();
+        MG_PP(P, 0);
+        space_step_coop(V, L, dt, lane, P);
+    }
+}
+
+template <int VAR, int BLK>
+__global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg, int max_steps,
+                                                  int auto_reset, const uint8_t *__restrict__ actions, float *reward,
+                                                  uint8_t *done, double *eval_score, uint8_t *reset_mask) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    constexpr StepCaps C = step_variant_caps(VAR);
+    constexpr bool LDS = VAR != 0;
+    constexpr bool COOP = VAR == 4;          // one env per workgroup of 64 lanes
+    constexpr int NCS = VAR >= 3 ? 0 : C.nc; // compile-time constraint list (0: the env's runtime list)
+    const int lane = COOP ? (int)threadIdx.x : BLK == 1 ? 0 : (int)threadIdx.x;
+    const int e = xcd_block(blockIdx.x, gridDim.x) * BLK + (COOP ? 0 : lane);
+    if (e >= S.n_envs) return;
+    const int a = actions[e];
+    MGProf P;
+    MG_PP_INIT(P);
+    if constexpr (LDS) {
+        if (S.nbodies[e] > C.nb || S.nshapes[e] > C.ns || S.ncons[e] > C.nc) {
+            S.overflow[e] |= 16; // scene larger than the variant's LDS caps (never expected)
+            if (reset_mask) reset_mask[e] = 0;
+            return;
+        }
+        bool ok = NCS == 0 || (S.ncons[e] == C.nc && S.robot_body0[e] == 0 && S.robot_cons0[e] == 0);
+        for (int c = 0; c < NCS; c++) {
+            const ConsDesc d = static_cons(c);
+            ok = ok && AT(S.ctype, c) == d.type && AT(S.ca, c) == d.a && AT(S.cb, c) == d.b;
+        }
+        if (!ok) { // the compiled constraint list does not describe this scene (never expected)
+            S.overflow[e] |= 32;
+            if (reset_mask) reset_mask[e] = 0;
+            return;
+        }
+        // the view is built from the LDS carve only (never merged with the HBM pointers), so every
+        // access through it compiles to ds_* with a constant offset from the lane's column
+        MGState V = S;
+        carve_view(V, smem, C, BLK);
+        if constexpr (COOP) {
+            xfer_state(S, V, C, 0, e, true, true, lane, 64);
+            __syncthreads();
+            env_substeps_coop(V, L, lane, a, P);
+            xfer_state(S, V, C, 0, e, false, true, lane, 64);
+            __syncthreads();
+            if (lane != 0) return;
+        } else {
+            xfer_state(S, V, C, lane, e, true, NCS == 0);
+            env_substeps<NCS>(V, L, lane, a, P);
+            xfer_state(S, V, C, lane, e, false);
+        }
+    } else {
+        env_substeps<0>(S, L, e, a, P);
+    }
+    int steps = S.episode_steps[e] + 1;
+    S.episode_steps[e] = steps;
+    bool d = max_steps > 0 && steps >= max_steps;
+    double sc = d ? score_env(S, L, e, cfg.task) : 0.0;
+    if (reward) reward[e] = (float)((cfg.flags & MG_DEBUG_REWARD) ? debug_reward(S, L, e, cfg.task) : sc);
+    if (done) done[e] = d ? 1 : 0;
+    if (eval_score) eval_score[e] = sc;
+    // VecEnv auto-reset (next obs = first frame of the new episode) runs as reset_kernel on this mask
+    if (reset_mask) reset_mask[e] = (d && auto_reset) ? 1 : 0;
+    MG_PP(P, 7);
+    MG_PP_END(P, (threadIdx.x & 63) == 0, 32);
+}
+
+template <int VAR, int BLK>
+hipError_t launch_step_var(const MGState &S, const mg_library *L, TaskCfg cfg, int max_steps, int auto_reset,
+                                  const uint8_t *actions, float *reward, uint8_t *done, double *eval_score,
+                                  uint8_t *reset_mask, hipStream_t st) {
+    constexpr StepCaps C = step_variant_caps(VAR);
+    const size_t lds = VAR == 0 ? 0 : mg_step_lds_bytes(C, BLK);
+    static bool attr_set = false;
+    if (VAR != 0 && !attr_set) {
+        hipError_t err = hipFuncSetAttribute((const void *)step_kernel<VAR, BLK>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (err != hipSuccess) return err;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((step_kernel<VAR, BLK>), dim3((S.n_envs + BLK - 1) / BLK), dim3(VAR == 4 ? 64 : BLK), lds, st, S, L, cfg,
+                       max_steps, auto_reset, actions, reward, done, eval_score, reset_mask);
+    return hipGetLastError();
+}

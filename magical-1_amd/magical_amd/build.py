@@ -1,6 +1,6 @@
 """Build the in-tree HIP library: python -m magical_amd.build [--force] [--profile]
 
-Three translation units compiled in parallel for gfx950 (hipcc
+Translation units compiled in parallel for gfx950 (hipcc
 --offload-arch=gfx950, -ffp-contract=off: no fused multiply-add except the
 explicit __fma_rn that reproduces numpy's BLAS arithmetic), then linked into
 magical_amd/libmagical_sim.so.  Objects are rebuilt only when their sources
@@ -18,9 +18,15 @@ OUT = os.path.join(HERE, "libmagical_sim.so")
 PROF_OUT = os.path.join(HERE, "libmagical_sim_prof.so")  # -DMG_PROFILE phase timers (tools/gpu_phase.py)
 _COMMON = ["mg_common.h", "mg_math.h", "mg_state.h", "mg_launch.h", "mg_prof.h"]
 _PHYS = _COMMON + ["mg_phys.h", "mg_step.h"]
-UNITS = {  # translation unit -> headers it depends on
+_STEP = _PHYS + ["mg_reset.h", "mg_score.h", "mg_stepk.h"]
+UNITS = {  # translation unit -> headers it depends on (one unit per kernel family: they compile in parallel)
     "mg_sim.hip": _COMMON + ["mg_phys.h"],
-    "mg_physics.hip": _PHYS + ["mg_reset.h", "mg_score.h"],
+    "mg_physics.hip": _COMMON,
+    "mg_reset.hip": _PHYS + ["mg_reset.h"],
+    "mg_step_robot.hip": _STEP,
+    "mg_step_v3.hip": _STEP,
+    "mg_step_v4.hip": _STEP,
+    "mg_step_hbm.hip": _STEP,
     "mg_raster.hip": _PHYS + ["mg_render.h"],
 }
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-Wno-unused-result"]

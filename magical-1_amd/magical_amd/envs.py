@@ -171,6 +171,12 @@ class VecMagicalEnv:
         native.check(self.lib.mg_random_actions(self.handle, ctypes.c_void_p(out.data_ptr()), key, step, self._stream()))
         return out
 
+    def set_episode_steps(self, steps):
+        """Overwrite every env's episode step counter (throughput runs stagger episode phases)."""
+        s = torch.as_tensor(steps).to(self.device, torch.int32).contiguous()
+        native.check(self.lib.mg_set_episode_steps(self.handle, ctypes.c_void_p(s.data_ptr()), self._stream()))
+        torch.cuda.current_stream(self.device).synchronize()
+
     def render_full(self, out=None):
         out = out if out is not None else torch.empty((self.num_envs, 2, 384, 384, 3), dtype=torch.uint8,
                                                       device=self.device)
@@ -204,6 +210,10 @@ class VecMagicalEnv:
             self.close()
         except Exception:
             pass
+
+
+class PlacementError(Exception):
+    """geom.py:111: raised by reset() when the layout randomiser gives up (after 10 retries)."""
 
 
 class MagicalEnv:
@@ -245,7 +255,10 @@ class MagicalEnv:
 
     def reset(self):
         self._episode_steps = 0
-        return self._np_obs(self._vec.reset())
+        obs = self._np_obs(self._vec.reset())
+        if int(self._vec.errors()[0].item()) & 2:  # pm_randomise_all_poses raised (geom.py:335-336)
+            raise PlacementError("could not place entities after 10 layout retries (geom.py:295-341)")
+        return obs
 
     def step(self, action):
         if self._episode_steps is None:

@@ -357,12 +357,14 @@ def star_verts(n_points, out_rad, in_rad):
     return out
 
 
-def make_circle_pts(radius, res):
-    """render.py:27-32"""
+def make_circle_pts(radius, res, trig=None):
+    """render.py:27-32.  trig = (cos, sin) replaces the correctly rounded pair (tests inject the
+    reference's libm values to show that is the only difference)."""
+    cos, sin = trig or (crcos, crsin)
     pts = []
     for i in range(res):
         ang = 2 * math.pi * i / res
-        pts.append((crcos(ang) * radius, crsin(ang) * radius))
+        pts.append((cos(ang) * radius, sin(ang) * radius))
     return pts
 
 
@@ -374,8 +376,9 @@ def make_rect_pts(width, height):
 
 # ---------------------------------------------------------------------------
 # render.py Transform (numpy arithmetic)
-def transform_trs(translation=(0.0, 0.0), rotation=0.0, scale=(1.0, 1.0)):
-    c, s = crcos(rotation), crsin(rotation)
+def transform_trs(translation=(0.0, 0.0), rotation=0.0, scale=(1.0, 1.0), trig=None):
+    cos, sin = trig or (crcos, crsin)
+    c, s = cos(rotation), sin(rotation)
     T = np.asarray([[1.0, 0.0, translation[0]], [0.0, 1.0, translation[1]], [0.0, 0.0, 1.0]])
     R = np.asarray([[c, -s, 0.0], [s, c, 0.0], [0.0, 0.0, 1.0]])
     S = np.asarray([[scale[0], 0.0, 0.0], [0.0, scale[1], 0.0], [0.0, 0.0, 1.0]])
@@ -395,13 +398,13 @@ def allo_view(res=384):
     return pygame_transform(res) @ cam
 
 
-def ego_view(rx, ry, ra, res=384):
+def ego_view(rx, ry, ra, res=384, trig=None):
     """base_env.py:309-316 + render.py:290-304, 349-371"""
     world_h = world_w = 2 * 1.02
     sx, sy = res / world_w, res / world_h
     scale = transform_trs(scale=(sx, sy))
     tr1 = transform_trs(translation=(world_w * 0.5, world_h * 0.15))
-    rot = transform_trs(rotation=-ra)
+    rot = transform_trs(rotation=-ra, trig=trig)
     tr2 = transform_trs(translation=(-rx, -ry))
     m = scale @ (tr1 @ (rot @ tr2))
     return pygame_transform(res) @ m

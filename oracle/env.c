@@ -16,6 +16,7 @@
 OEnv *oenv_create(int task, int flags, int preproc, int max_steps, uint32_t seed) {
     OEnv *e = (OEnv *)calloc(1, sizeof(OEnv));
     e->task = task; e->flags = flags; e->preproc = preproc; e->max_steps = max_steps;
+    e->max_tries = 10000;
     o_mt_seed(&e->rng, seed);
     return e;
 }
@@ -82,6 +83,7 @@ static void render_both(OEnv *e, uint8_t *allo384, uint8_t *ego384) {
 
 int oenv_reset(OEnv *e, uint8_t *obs) {
     e->placement_error = 0;
+    e->placement_retries = 0;
     oscene_reset(e);
     uint8_t *a = (uint8_t *)malloc((size_t)O_RES * O_RES * 3), *g = (uint8_t *)malloc((size_t)O_RES * O_RES * 3);
     render_both(e, a, g);
@@ -178,3 +180,6 @@ void oenv_get_phys_vars(const OEnv *e, double out[5]) {
 void o_palette(uint8_t out[5][4][3]) { memcpy(out, O_PALETTE, sizeof(O_PALETTE)); }
 
 void o_downsample(const uint8_t *frame384, uint8_t *out96) { oraster_downsample(frame384, out96); }
+
+int oenv_placement_retries(const OEnv *e) { return e->placement_retries; }
+void oenv_set_max_tries(OEnv *e, int n) { e->max_tries = n > 0 ? n : 10000; }

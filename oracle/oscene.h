@@ -50,6 +50,8 @@ struct OEnv {
     double pv[5]; /* PhysicsVariables: robot_pos, robot_rot, finger, shape_trans, shape_rot */
     double target_speed, rel_turn, target_finger;
     int episode_steps;
+    int max_tries;         /* geom.py:198 max_tries = 10000 (tests lower it to force retries) */
+    int placement_retries; /* failed pm_randomise_all_poses retries in the last reset (tests only) */
     int placement_error; /* geom.py:335-336: PlacementError after max_retries */
     double last_score;
     /* PickAndPlace (pick_and_place.py:30-85): target shape entity, ids, position */

@@ -44,6 +44,8 @@ def lib():
         L.oenv_render_full.argtypes = [vp, vp, vp]
         L.oenv_get_bodies.restype = i; L.oenv_get_bodies.argtypes = [vp, vp, i]
         L.oenv_num_arbiters.restype = i; L.oenv_num_arbiters.argtypes = [vp]
+        L.oenv_placement_retries.restype = i; L.oenv_placement_retries.argtypes = [vp]
+        L.oenv_set_max_tries.argtypes = [vp, i]
         L.oenv_get_entities.restype = i; L.oenv_get_entities.argtypes = [vp, vp, vp, vp, vp]
         L.o_mt_seed.argtypes = [vp, u32]
         L.o_mt_next32.restype = u32; L.o_mt_next32.argtypes = [vp]
@@ -170,6 +172,14 @@ class OracleEnv:
         out = np.zeros(5)
         self.L.oenv_get_phys_vars(self.h, ptr(out))
         return out
+
+    def set_max_tries(self, n):
+        """pm_randomise_pose max_tries (geom.py:198, 10000); lowered by tests to force layout retries"""
+        self.L.oenv_set_max_tries(self.h, int(n))
+
+    def placement_retries(self):
+        """failed whole-layout retries of pm_randomise_all_poses in the last reset (geom.py:295-341)"""
+        return self.L.oenv_placement_retries(self.h)
 
     def num_arbiters(self):
         return self.L.oenv_num_arbiters(self.h)

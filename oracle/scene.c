@@ -642,7 +642,7 @@ static int randomise_pose(OEnv *e, OEntity *en, int rand_pos, int rand_rot, doub
     }
     double rmin = -M_PI, rmax = M_PI;
     if (rot_limit >= 0) { rmin = orig_angle - rot_limit; rmax = orig_angle + rot_limit; }
-    for (int tries = 0; tries < 10000; tries++) {
+    for (int tries = 0; tries < e->max_tries; tries++) {
         vec2 npos = orig_pos;
         if (rand_pos) {
             double x = o_mt_uniform(&e->rng, xlo, xhi);
@@ -682,6 +682,7 @@ static void randomise_all_poses_ign(OEnv *e, const int *ents, int n, const int *
             if (randomise_pose(e, en, 1, rand_rot[k], pos_limit, rot_limits[k], ign) != 0) { failed = 1; break; }
         }
         if (!failed) return;
+        e->placement_retries++; /* test instrumentation: failed whole-layout retries of this reset */
     }
     e->placement_error = 1;
 }

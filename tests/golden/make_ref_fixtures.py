@@ -1,0 +1,180 @@
+"""Golden fixtures computed by EXECUTING the reference's own pure numpy/math code
+(run in the dev container, where /root/reference exists; the GPU box only reads
+the JSON output).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_ref_fixtures.py
+
+The reference package cannot be imported here (pygame / pymunk / gym / cv2 are
+absent: ModuleNotFoundError, not a permission denial), so the functions below are
+taken out of the reference source files with `ast` and executed in a namespace
+that supplies numpy, math, itertools and inert stand-ins for the two pygame-bound
+names they mention but do not use for arithmetic (`Poly` records its points,
+`pygame.Surface` is never drawn on).  Nothing of the reference's source text is
+written out: the JSON files hold inputs and the reference's outputs only.
+
+  * ref_render.json  -- render.py:13-35 (make_rect, make_circle), :37-124
+                        (Transform, incl. rigid_transform), :127-138 (Stack),
+                        :290-304 (ego_cam_matrix), :307-371 (Viewer.set_bounds,
+                        Viewer.set_cam_follow) with base_env.py:309-322's camera
+                        arguments and style.py's ARENA_ZOOM_OUT; the libm sin/cos
+                        the reference's math.sin/cos returned are stored beside
+                        each case.
+  * ref_make_line.json -- benchmarks/make_line.py:31-72 (longest_line) on random
+                        point sets and on near-collinear sets that sit at the
+                        scorer's inlier / separation thresholds.
+"""
+import ast
+import importlib.util
+import itertools
+import json
+import math
+import os
+import sys
+import types
+import typing
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference/magical"
+sys.dont_write_bytecode = True
+
+
+def _extract(path, names, namespace):
+    """Execute the top-level definitions `names` of the reference file `path` in `namespace`."""
+    tree = ast.parse(open(path).read(), filename=path)
+    nodes = [n for n in tree.body if isinstance(n, (ast.FunctionDef, ast.ClassDef)) and n.name in names]
+    missing = set(names) - {n.name for n in nodes}
+    assert not missing, missing
+    mod = ast.Module(body=nodes, type_ignores=[])
+    exec(compile(mod, path, "exec"), namespace)
+    return namespace
+
+
+class _Poly:
+    """stand-in for render.Poly: keeps the points and the outline flag"""
+
+    def __init__(self, points, outline):
+        self.points, self.outline, self.dashed = [tuple(map(float, p)) for p in points], outline, False
+
+
+class _Geom:
+    @staticmethod
+    def convert_color(*rgb):
+        return rgb
+
+
+def _render_namespace():
+    ns = {"__name__": "ref_render", "np": np, "math": math, "dataclasses": __import__("dataclasses"),
+          "abc": __import__("abc"), "List": typing.List, "Tuple": typing.Tuple, "Union": typing.Union,
+          "Poly": _Poly, "Geom": _Geom,
+          "pygame": types.SimpleNamespace(Surface=lambda *a, **k: None)}
+    ns["CoordType"] = typing.Union[typing.Tuple[float, float], typing.List[float], np.ndarray]
+    ns["ArrayLike"] = typing.Union[typing.List[ns["CoordType"]], typing.Tuple[ns["CoordType"]]]
+    return _extract(os.path.join(REF, "render.py"),
+                    ["make_rect", "make_circle", "make_square", "Transform", "Stack", "ego_cam_matrix", "Viewer"], ns)
+
+
+def _zoom_out():
+    spec = importlib.util.spec_from_file_location("ref_style", os.path.join(REF, "style.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.ARENA_ZOOM_OUT
+
+
+def _m(a):
+    return np.asarray(a, dtype=np.float64).ravel().tolist()
+
+
+def ref_render():
+    R = _render_namespace()
+    Z = _zoom_out()
+    rs = np.random.RandomState(2024)
+    out = {"arena_zoom_out": Z, "res": 384}
+    # base_env.py:318-322: the arena is [-1, 1]^2
+    v = R["Viewer"](384, 384)
+    v.set_bounds(left=-1 * Z, right=1 * Z, bottom=-1 * Z, top=1 * Z)
+    out["allo_view"] = _m(v.transform.matrix)
+    out["pygame_transform"] = _m(v.pygame_transform.matrix)
+    ego = []
+    angles = list(rs.uniform(-7, 7, 300)) + [0.0, -2.13, 0.83693, -1.2 * math.pi, 0.55 * math.pi, 3.83, 0.347,
+                                             0.718, math.pi, -math.pi, 1e-9, -3.7e-5]
+    for a in angles:
+        x, y = rs.uniform(-1.1, 1.1, 2)
+        v.set_cam_follow(source_xy_world=(x, y), target_xy_01=(0.5, 0.15), viewport_hw_world=(2 * Z, 2 * Z),
+                         rotation=float(a))
+        ego.append({"x": float(x), "y": float(y), "a": float(a), "m": _m(v.transform.matrix),
+                    "libm_sin": math.sin(-float(a)), "libm_cos": math.cos(-float(a))})
+    out["ego_view"] = ego
+    trs = []
+    for _ in range(200):
+        t = rs.uniform(-400, 400, 2)
+        r = float(rs.uniform(-7, 7))
+        s = rs.uniform(-200, 200, 2)
+        tr = R["Transform"](translation=(float(t[0]), float(t[1])), rotation=r, scale=(float(s[0]), float(s[1])))
+        trs.append({"t": _m(t), "r": r, "s": _m(s), "m": _m(tr.matrix), "libm_sin": math.sin(r),
+                    "libm_cos": math.cos(r)})
+    out["transform"] = trs
+    stacks = []
+    for _ in range(60):
+        st = R["Stack"]()
+        mats = []
+        for _k in range(int(rs.randint(1, 5))):
+            m = rs.uniform(-3, 3, (3, 3))
+            m[2] = (0.0, 0.0, 1.0)
+            st.push(R["Transform"].from_matrix(m))
+            mats.append(_m(m))
+        pts = rs.uniform(-1.5, 1.5, (6, 2))
+        stacks.append({"mats": mats, "top": _m(st.stack[-1]), "pts": _m(pts),
+                       "pts_out": _m(st.apply_current_matrix(pts))})
+    out["stack"] = stacks
+    # render.py polygons used by entities.py: make_circle(r, 100) for the robot body / eye / pupil and the
+    # circle block, make_rect for the arena and goal regions, make_square for the square block
+    circles = []
+    for radius in (0.2, 0.2 * 0.2, 0.12 * 0.2, 0.2 * 0.6):
+        p = R["make_circle"](radius, 100, True)
+        circles.append({"radius": radius, "res": 100, "pts": [list(q) for q in p.points],
+                        "libm": [[math.cos(2 * math.pi * i / 100), math.sin(2 * math.pi * i / 100)]
+                                 for i in range(100)]})
+    out["circle"] = circles
+    rects = []
+    for w, h in [(2.0, 2.0), (0.75, 0.76), (0.6, 0.7), (0.72, 0.67), (0.427, 0.468)] + \
+            [tuple(rs.uniform(0.4, 0.8, 2)) for _ in range(8)]:
+        rects.append({"w": float(w), "h": float(h), "pts": [list(q) for q in R["make_rect"](float(w), float(h), True).points]})
+    out["rect"] = rects
+    side = math.sqrt(math.pi) * 0.2 * 0.6
+    out["square"] = {"side": side, "pts": [list(q) for q in R["make_square"](side, True).points]}
+    return out
+
+
+def ref_make_line():
+    ns = _extract(os.path.join(REF, "benchmarks", "make_line.py"), ["longest_line"],
+                  {"__name__": "ref_make_line", "np": np, "it": itertools})
+    longest_line = ns["longest_line"]
+    rs = np.random.RandomState(0)
+    shape_rad = 0.2 * 0.6
+    inlier, sep = shape_rad * 1.5, shape_rad * 3.5   # make_line.py: inlier_dist / max_sep defaults
+    cases = [rs.uniform(-1, 1, (rs.randint(1, 5), 2)) for _ in range(700)]
+    for _ in range(900):  # points near a random line, spacing around the separation threshold
+        n = rs.randint(3, 5)
+        o, d = rs.uniform(-0.5, 0.5, 2), rs.uniform(-1, 1, 2)
+        d /= np.linalg.norm(d)
+        t = np.cumsum(rs.uniform(0.3, 0.5, n))
+        off = rs.uniform(-1, 1, n) * rs.choice([0.0, 0.17, 0.18, 0.19])
+        cases.append(o + t[:, None] * d + off[:, None] * np.array([-d[1], d[0]]))
+    out = []
+    for p in cases:
+        out.append({"pts": p.ravel().tolist(), "best": int(longest_line(p, inlier, sep))})
+    return {"inlier_dist": inlier, "max_sep": sep, "cases": out}
+
+
+def main():
+    for fn, data in (("ref_render.json", ref_render()), ("ref_make_line.json", ref_make_line())):
+        with open(os.path.join(HERE, fn), "w") as f:
+            json.dump(data, f, indent=None, separators=(",", ":"))
+            f.write("\n")
+        print("wrote", fn)
+
+
+if __name__ == "__main__":
+    main()

@@ -532,3 +532,72 @@ def test_batched_evaluation_protocol():
 
     frame = Checked("MoveToRegion-Demo-LoRes4E-v0", n, policy, run_id="random").do_eval()
     assert len(frame) == 1 + len(registry.DEMO_ENVS_TO_TEST_ENVS_MAP["MoveToRegion-Demo-LoRes4E-v0"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["MatchRegions-TestAll-LoRes4E-v0", "FindDupe-TestAll-LoRes4E-v0",
+                                  "FixColour-TestAll-LoRes4E-v0", "ClusterColour-TestAll-LoResStack-v0",
+                                  "MakeLine-TestAll-LoRes4E-v0"])
+def test_layout_retry_parity(name, monkeypatch):
+    """pm_randomise_all_poses retries (geom.py:295-341) with the try budget of pm_randomise_pose
+    lowered from 10000 to 3 on both sides (MG_DEBUG_MAX_TRIES / OracleEnv.set_max_tries), so most
+    seeds need >= 1 failed whole-layout retry (seeds found by tools/scan_retry_seeds.py).  Covers:
+    each entity's filter captured per retry (entities left with categories 0 by a failed retry stay
+    non-colliding, in placement, physics and goal queries), rollback to the saved absolute poses on
+    PlacementError, and the PlacementError flag.  Episodes cross an auto-reset (max_episode_steps 12)."""
+    monkeypatch.setenv("MG_DEBUG_MAX_TRIES", "3")
+    spec = registry.lookup(name)
+    n, steps, L = 48, 26, 12
+    seeds = list(range(n))
+    vec = magical_amd.make_vec(name, n, seeds=seeds, max_episode_steps=L)
+    orc = []
+    for s in seeds:
+        o = po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, L, seed=s)
+        o.set_max_tries(3)
+        orc.append(o)
+    placement = np.zeros(n, dtype=bool)
+    retried = 0
+    obs = vec.reset()
+    ref = []
+    for i, o in enumerate(orc):
+        try:
+            ref.append(oracle_obs_split(spec, o.reset()))
+        except po.PlacementError:
+            placement[i] = True
+            ref.append(None)
+            continue
+        retried += o.placement_retries() > 0
+    assert retried >= n // 4, f"only {retried} of {n} seeds exercised a layout retry"
+    errs = vec.errors().cpu().numpy()
+    assert np.array_equal((errs & 2) != 0, placement)
+    live = [i for i in range(n) if not placement[i]]
+    for k in obs:
+        got = obs[k].cpu().numpy()
+        for i in live:
+            assert np.array_equal(got[i], ref[i][k]), f"reset obs {k} env {i}"
+    acts = np.random.RandomState(6).randint(0, 18, (steps, n))
+    for t in range(steps):
+        obs, rew, done, info = vec.step(torch.as_tensor(acts[t], dtype=torch.uint8))
+        got = {k: v.cpu().numpy() for k, v in obs.items()}
+        got_done, got_score = done.cpu().numpy(), info["eval_score"].cpu().numpy()
+        bodies = vec.bodies()[0].cpu().numpy()
+        errs = vec.errors().cpu().numpy()
+        for i in live:
+            if placement[i]:
+                continue
+            o, r, d, s = orc[i].step(int(acts[t, i]))
+            assert bool(got_done[i]) == d and got_score[i] == s, f"step {t} env {i} score {got_score[i]} vs {s}"
+            if d:
+                try:
+                    o = orc[i].reset()
+                except po.PlacementError:
+                    placement[i] = True
+                    assert errs[i] & 2, f"step {t} env {i}: PlacementError on the oracle only"
+                    continue
+            else:
+                b = orc[i].bodies()
+                assert np.abs(bodies[i, :len(b)] - b).max() <= POSE_TOL, f"step {t} env {i} bodies"
+            ref_i = oracle_obs_split(spec, o)
+            for k in got:
+                assert np.array_equal(got[k][i], ref_i[k]), f"step {t} env {i} obs {k}"
+    vec.close()

@@ -24,6 +24,6 @@ for s in range(20):
     vec.random_actions(100 + s, out=acts)
     vec.step(acts)
 torch.cuda.synchronize()
-tm = (ctypes.c_double * 3)()
+tm = (ctypes.c_double * 4)()
 native.check(lib.mg_read_timing(vec.handle, tm))
 print(f"step {tm[0] / 20:.3f} ms render {tm[1] / 20:.3f} ms")
