@@ -168,8 +168,9 @@ static int np_arange(double start, double stop, double step, double *out, int ma
     return len;
 }
 
-/* render.py:230-255 dashed branch */
-static void draw_dashed(uint8_t *fr, double x1, double y1, double x2, double y2, const uint8_t *c) {
+/* render.py:230-255 dashed branch: the (start, end) integer endpoints of each
+ * pygame.draw.line(..., 4) call, in call order; returns the number of dashes */
+static int dash_segments(double x1, double y1, double x2, double y2, int *seg, int maxseg) {
     double xs[512], ys[512];
     int nx, ny;
     const double dl = 10;
@@ -188,16 +189,21 @@ static void draw_dashed(uint8_t *fr, double x1, double y1, double x2, double y2,
         nx = np_arange(x1, x2, x1 < x2 ? dx : -dx, xs, 512);
         ny = np_arange(y1, y2, y1 < y2 ? dy : -dy, ys, 512);
     }
-    int n = nx < ny ? nx : ny;
+    int n = nx < ny ? nx : ny, k;
     /* next = odd indices, last = even indices; zip truncates */
-    for (int k = 0; 2 * k + 1 < n; k++) {
-        int pts[4];
-        pts[0] = (int)nearbyint(xs[2 * k + 1]);
-        pts[1] = (int)nearbyint(ys[2 * k + 1]);
-        pts[2] = (int)nearbyint(xs[2 * k]);
-        pts[3] = (int)nearbyint(ys[2 * k]);
-        clip_and_draw_line_width(fr, c, 4, pts);
+    for (k = 0; 2 * k + 1 < n && k < maxseg; k++) {
+        seg[4 * k + 0] = (int)nearbyint(xs[2 * k + 1]);
+        seg[4 * k + 1] = (int)nearbyint(ys[2 * k + 1]);
+        seg[4 * k + 2] = (int)nearbyint(xs[2 * k]);
+        seg[4 * k + 3] = (int)nearbyint(ys[2 * k]);
     }
+    return k;
+}
+
+static void draw_dashed(uint8_t *fr, double x1, double y1, double x2, double y2, const uint8_t *c) {
+    int seg[4 * 256];
+    int n = dash_segments(x1, y1, x2, y2, seg, 256);
+    for (int k = 0; k < n; k++) clip_and_draw_line_width(fr, c, 4, seg + 4 * k);
 }
 
 static void render_geom(const OEnv *e, const OGeom *g, const double *view, uint8_t *fr) {
@@ -255,4 +261,12 @@ void oraster_downsample(const uint8_t *in, uint8_t *out) {
                 int q = s >> 4, r = s & 15;
                 out[((size_t)oy * O_LORES + ox) * 3 + ch] = (uint8_t)(q + (r > 8 || (r == 8 && (q & 1))));
             }
+}
+
+/* ---- pieces exported for the raster known-answer tests (tests/test_oracle_known_answers.py) ---- */
+void o_fill_poly(uint8_t *fr, const int *vx, const int *vy, int n, const uint8_t *c) { fill_poly(fr, vx, vy, n, c); }
+int o_clipline(int *pts) { return clipline(pts, 0, 0, W - 1, H - 1); }
+void o_line_width(uint8_t *fr, const uint8_t *c, int width, const int *pts) { clip_and_draw_line_width(fr, c, width, pts); }
+int o_dash_segments(double x1, double y1, double x2, double y2, int *seg, int maxseg) {
+    return dash_segments(x1, y1, x2, y2, seg, maxseg);
 }

@@ -19,6 +19,12 @@ written out: the JSON files hold inputs and the reference's outputs only.
                         arguments and style.py's ARENA_ZOOM_OUT; the libm sin/cos
                         the reference's math.sin/cos returned are stored beside
                         each case.
+  * ref_outline.json -- render.py:202-287 (Poly._render, Poly.draw_outline): the
+                        pygame.draw.polygon / lines / line calls the reference makes
+                        (points, width) for solid and dashed outlines, recorded by a
+                        stand-in pygame.draw on pixel-space polygons (goal
+                        rectangles through allo and ego views, random quads, exact
+                        axis-aligned and .5-tie edges).
   * ref_make_line.json -- benchmarks/make_line.py:31-72 (longest_line) on random
                         point sets and on near-collinear sets that sit at the
                         scorer's inlier / separation thresholds.
@@ -147,6 +153,74 @@ def ref_render():
     return out
 
 
+class _Recorder:
+    """stand-in for pygame.draw: records each call's points and width"""
+
+    def __init__(self):
+        self.calls = []
+
+    def polygon(self, surface, color, points, width=0):
+        self.calls.append(["polygon", [[float(c) for c in p] for p in points], width])
+
+    def lines(self, surface, color, closed, points, width=1):
+        self.calls.append(["lines", [[float(c) for c in p] for p in points], width, bool(closed)])
+
+    def line(self, surface, color, start, end, width=1):
+        self.calls.append(["line", [[float(c) for c in start], [float(c) for c in end]], width])
+
+    def circle(self, surface, color, pos, radius, width=0):
+        self.calls.append(["circle", [[float(c) for c in pos]], radius])
+
+
+def ref_outline():
+    rec = _Recorder()
+
+    class _GeomBase:
+        def __init__(self):
+            self._color = (1, 2, 3, 1)
+            self._outline_color = (4, 5, 6, 1)
+
+    ns = {"__name__": "ref_outline", "np": np, "math": math, "abc": __import__("abc"), "Geom": _GeomBase,
+          "pygame": types.SimpleNamespace(Surface=object, draw=rec)}
+    ns["ArrayLike"] = typing.Any
+    _extract(os.path.join(REF, "render.py"), ["Poly"], ns)
+    Poly = ns["Poly"]
+    R = _render_namespace()
+    Z = _zoom_out()
+    rs = np.random.RandomState(77)
+    polys = []
+    v = R["Viewer"](384, 384)
+    for k in range(160):
+        w, h = rs.uniform(0.4, 0.8, 2)
+        x, y = rs.uniform(-1.0, 1.0 - w), rs.uniform(-1.0 + h, 1.0)
+        corners = np.array(R["make_rect"](float(w), float(h), True).points) + np.array([x + w / 2, y - h / 2])
+        if k % 2 == 0:
+            v.set_bounds(left=-1 * Z, right=1 * Z, bottom=-1 * Z, top=1 * Z)
+        else:
+            rx, ry = rs.uniform(-1, 1, 2)
+            v.set_cam_follow(source_xy_world=(float(rx), float(ry)), target_xy_01=(0.5, 0.15),
+                             viewport_hw_world=(2 * Z, 2 * Z), rotation=float(rs.uniform(-7, 7)))
+        st = R["Stack"]()
+        st.push(v.pygame_transform)
+        st.push(v.transform)
+        polys.append(st.apply_current_matrix(corners))
+    for _ in range(40):
+        polys.append(rs.uniform(-60, 444, (4, 2)))
+    polys.append(np.array([[10.0, 20.0], [200.0, 20.0], [200.0, 300.5], [10.0, 300.5]]))
+    polys.append(np.array([[-30.5, 5.5], [420.5, 5.5], [420.5, 390.0], [-30.5, 390.0]]))
+    polys.append(np.array([[17.5, 12.5], [372.5, 33.5], [352.5, 371.5], [27.5, 342.5]]))
+    out = []
+    for pts in polys:
+        for dashed in (True, False):
+            p = Poly(pts.tolist(), True)
+            p.dashed = dashed
+            p.geom = np.asarray(pts, dtype=np.float64)
+            rec.calls = []
+            p._render(None)
+            out.append({"pts": _m(pts), "dashed": dashed, "calls": rec.calls})
+    return {"cases": out}
+
+
 def ref_make_line():
     ns = _extract(os.path.join(REF, "benchmarks", "make_line.py"), ["longest_line"],
                   {"__name__": "ref_make_line", "np": np, "it": itertools})
@@ -169,7 +243,8 @@ def ref_make_line():
 
 
 def main():
-    for fn, data in (("ref_render.json", ref_render()), ("ref_make_line.json", ref_make_line())):
+    for fn, data in (("ref_render.json", ref_render()), ("ref_make_line.json", ref_make_line()),
+                     ("ref_outline.json", ref_outline())):
         with open(os.path.join(HERE, fn), "w") as f:
             json.dump(data, f, indent=None, separators=(",", ":"))
             f.write("\n")

@@ -15,7 +15,7 @@ mkdir -p "$OUT"
 export PYTHONDONTWRITEBYTECODE=1
 
 if [ "$MODE" = "pytest" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
   rc=$?; echo "pytest -m gpu rc=$rc"; tail -5 "$OUT/pytest_gpu.log"
   [ $rc -eq 0 ] || exit $rc
 fi
