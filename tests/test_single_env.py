@@ -50,9 +50,11 @@ def _oracle_obs(spec, flat, orc):
         n = int(np.prod(s))
         ref[k] = flat[off:off + n].reshape(s)
         off += n
-    if spec.task == "PickAndPlace":  # pick_and_place.py:103-107: ints and a float64 pair
-        t = orc.target()
-        ref["target_type"], ref["target_colour"], ref["target_position"] = int(t[0]), int(t[1]), t[2:4]
+    if spec.task == "PickAndPlace":  # pick_and_place.py:103-107: ints and a float64 pair, after allo/ego
+        t = orc.target()          # and before the frame stack's past_obs (benchmarks/__init__.py:136,146)
+        extra = [("target_type", int(t[0])), ("target_colour", int(t[1])), ("target_position", t[2:4])]
+        items = list(ref.items())
+        ref = collections.OrderedDict(items[:2] + extra + items[2:])
     return ref
 
 

@@ -2,7 +2,7 @@
 # One GPU-box session: parity tests, bench line, rocprofv3 kernel-trace stats
 # and the two PMC passes (FETCH_SIZE / WRITE_SIZE cannot share a pass).
 # Usage (from the dev container):
-#   gpurun --timeout 1200 -- 'bash tools/gpu_round.sh <tag> [pytest|nopytest] [bench args...]'
+#   gpurun --timeout 1200 -- 'bash tools/gpu_round.sh <tag> [pytest|nopytest|<test path>] [bench args...]'
 set -u
 TAG=${1:-r01}
 MODE=${2:-pytest}
@@ -14,8 +14,9 @@ OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
 export PYTHONDONTWRITEBYTECODE=1
 
-if [ "$MODE" = "pytest" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+if [ "$MODE" != "nopytest" ]; then
+  TESTS=tests; [ "$MODE" = "pytest" ] || TESTS="$MODE"
+  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
   rc=$?; echo "pytest -m gpu rc=$rc"; tail -5 "$OUT/pytest_gpu.log"
   [ $rc -eq 0 ] || exit $rc
 fi
@@ -36,5 +37,9 @@ rc=$?; echo "pmc fetch rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$OUT/pmc_fetch.log"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run -- \
   python "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline $BARGS > "$OUT/pmc_write.log" 2>&1
 rc=$?; echo "pmc write rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$OUT/pmc_write.log"; exit $rc; }
+
+timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$OUT/pmc_sq" -o run -- \
+  python "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline $BARGS > "$OUT/pmc_sq.log" 2>&1
+rc=$?; echo "pmc sq rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$OUT/pmc_sq.log"; exit $rc; }
 find "$OUT" -name "*.csv" | head -20
 exit 0
