@@ -54,6 +54,21 @@ MG_DEV void body_set_angle(const MGState &S, int e, int b, double a) {
     }
 }
 
+// Bodies whose rotation transform nothing reads: the robot's kinematic control body (its one joint,
+// PivotJoint(control, body, (0, 0), (0, 0)) at entities.py:312-320, rotates a zero anchor, so any
+// rotation gives the same r1) and its two eye bodies (no shapes; their DampedRotarySprings read angles,
+// not transforms; the pupils are drawn from angle differences, entities.py:489-491).  Their angle is
+// stored without the correctly rounded sincos: the cache (bacache) then no longer matches the angle and
+// any reader that needs the transform recomputes it (render body_sincos).
+MG_DEV bool body_rot_unused(const MGState &S, int e, int b) {
+    const int r = S.robot_body0[e];
+    return b > r && b <= r + 3;
+}
+MG_DEV void body_set_angle_step(const MGState &S, int e, int b, double a) {
+    if (body_rot_unused(S, e, b)) AT(S.ba, b) = a;
+    else body_set_angle(S, e, b, a);
+}
+
 // --------------------------------------------------------------------------
 // world-space view of one shape (cpShape cache data)
 enum { WS_CIRCLE = 0, WS_SEGMENT = 1, WS_POLY = 2 };

@@ -21,10 +21,10 @@
 #include "mg_prof.h"
 
 // capacity classes (template parameters of the LDS layout): geoms, vertices, dash lines, bin entries
-// (outline items + fill edges, binned per band).  The large class fits every task; the small one fits
+// (outline items + fill edges, binned per band), solid outline edges.  The large class fits every task; the small one fits
 // robot + arena + goal + one block (MoveToRegion / MoveToCorner) and leaves room for 5 workgroups/CU.
-#define RG_LARGE 160, 1600, 256, 3072
-#define RG_SMALL 32, 704, 160, 1536
+#define RG_LARGE 160, 1600, 256, 3072, 1600
+#define RG_SMALL 32, 704, 160, 1536, 256
 #define RG_MAXLONG 16
 #define RG_BAND 8
 #define RG_NBANDS (MG_RES / RG_BAND)
@@ -36,6 +36,18 @@
 #define RG_BANDLO (2 * RG_LOROW)        // bytes of the 2 LoRes rows one band produces
 #define RG_BANDLO16 (RG_BANDLO / 16)    // ... in 16-byte chunks (36)
 
+// q = n / d and r = n % d for 0 <= n < 2^31, 1 <= d: a float reciprocal estimate (relative error below
+// 2^-22, so q is off by at most one for n < 2^22) corrected by one step; larger n take the integer divide
+MG_DEV int udivmod(int n, int d, int &r) {
+    int q;
+    if (n >= (1 << 22)) q = n / d;
+    else q = (int)((float)n * __builtin_amdgcn_rcpf((float)d));
+    r = n - q * d;
+    if (r < 0) { q--; r += d; }
+    else if (r >= d) { q++; r -= d; }
+    return q;
+}
+
 // A pygame drawline pixel run in k-form: the major axis has n = max(|dx|,|dy|) + 1
 // pixels and the minor offset of pixel k is m = floor(k * dminor / dmajor) with
 // DX = |dx| + 1, DY = |dy| + 1 (horizontal and vertical lines are the cases
@@ -43,16 +55,24 @@
 // y-major: (x1 + sgx*m, y1 + sgy*k).
 struct LineK { int x1, y1, sgx, sgy, DX, DY, xmaj; };
 
-// LDS: the setup matrices and the band buffers are never live at the same time,
-// so they share storage.  Sized for 3 workgroups per CU.
-template <int MAXG_, int MAXVERT_, int MAXDASH_, int MAXBIN_>
+// LDS: the setup matrices / scratch and the band buffers are never live at the same time, so they
+// share storage.  Small class: 6 workgroups per CU (<= 26 KiB); large class: 3.
+template <int MAXG_, int MAXVERT_, int MAXDASH_, int MAXBIN_, int MAXSEDGE_>
 struct RenderSmem {
-    static constexpr int RG_MAXG = MAXG_, RG_MAXVERT = MAXVERT_, RG_MAXDASH = MAXDASH_, RG_MAXBIN = MAXBIN_;
+    static constexpr int RG_MAXG = MAXG_, RG_MAXVERT = MAXVERT_, RG_MAXDASH = MAXDASH_, RG_MAXBIN = MAXBIN_,
+                         RG_MAXSEDGE = MAXSEDGE_;
     union alignas(16) {
         struct {
             double g_m[RG_MAXG][6];
             double e_xf[MG_MAX_ENTS][5][9];
             double view[9];
+            // setup scratch (dead before the bands)
+            int32_t gbb[RG_MAXG][4];                 // per-geom ymin, ymax, xmin, xmax while built (atomics)
+            int32_t gchg[RG_MAXG];                   // direction changes of the y sequence around each polygon
+            int32_t bin_cnt[RG_NBANDS], ebin_cnt[RG_NBANDS];
+            int16_t g_rpoly[RG_MAXG];
+            int8_t g_ent[RG_MAXG];
+            int16_t e_g0[MG_MAX_ENTS + 1];
         } pre;
         struct {
             uint32_t band[RG_BAND][MG_RES]; // outline layer of the current band
@@ -61,24 +81,20 @@ struct RenderSmem {
             int32_t lkr[RG_MAXLONG][3];     // klo, khi, ordinal
         } post;
     } u;
-    uint4 ginfo[RG_MAXG];                     // (ymin|ymax<<16, xmin|xmax<<16, -, -); int32 atomics while built
-    int32_t gchg[RG_MAXG];                    // direction changes of the y sequence around each polygon
+    uint2 ginfo[RG_MAXG];                     // (ymin | ymax << 16, xmin | xmax << 16), int16 halves
     uint32_t bspan[RG_MAXG][RG_BAND];         // spans of the band's rows, per band-list slot: l | r << 16
     uint64_t col[2 * RG_MAXG + 2];            // R | G << 16 | B << 32 per ordinal
-    int16_t g_rpoly[RG_MAXG], g_voff[RG_MAXG + 1], g_nv[RG_MAXG];
-    int8_t g_ent[RG_MAXG];
-    int16_t e_g0[MG_MAX_ENTS + 1];
+    int16_t g_voff[RG_MAXG + 1], g_nv[RG_MAXG];
     int16_t vx[RG_MAXVERT], vy[RG_MAXVERT];   // int pixel vertices (pygame (int) truncation)
     uint8_t fdelta[RG_MAXVERT];               // float->int minus double->int of x (bits 0-1) / y (2-3), +1
     uint8_t v_geom[RG_MAXVERT];
-    uint16_t sedge[RG_MAXVERT];               // solid outline edges: start vertex | last << 14 | inside << 15
+    uint16_t sedge[RG_MAXSEDGE];              // solid outline edges: start vertex | last << 14 | inside << 15
     int16_t blist[RG_MAXG];                   // geoms overlapping the current band, in draw order
     int16_t dash[RG_MAXDASH][4];              // clipped dashed-outline lines
     int16_t dash_o[RG_MAXDASH];
     int16_t bin_off[RG_NBANDS + 1];           // per-band outline item lists (in bin[])
     int16_t ebin_off[RG_NBANDS + 1];          // per-band fill edge lists (in bin[], after the outline items)
-    int32_t bin_cnt[RG_NBANDS], ebin_cnt[RG_NBANDS];
-    int16_t bin[RG_MAXBIN];
+    uint16_t bin[RG_MAXBIN];                  // outline item index, or fill edge: vertex | closing << 14 | last-row << 15
     int16_t gslot[RG_MAXG];                   // band-list slot of each geom overlapping the current band
     int32_t ngeom, nsedge, ndash, nlong, nblist, err;
 #ifdef MG_PROFILE
@@ -238,8 +254,9 @@ MG_DEV void band_krange(const LineK &L, int y0, int &klo, int &khi) {
     mlo = mlo > 0 ? mlo : 0;
     mhi = mhi < L.DY - 1 ? mhi : L.DY - 1;
     if (L.xmaj) {
-        const int kl = (mlo * L.DX + L.DY - 1) / L.DY;            // smallest k with k*DY >= mlo*DX
-        const int kh = ((mhi + 1) * L.DX + L.DY - 1) / L.DY - 1;  // largest k with k*DY < (mhi+1)*DX
+        int rem;
+        const int kl = udivmod(mlo * L.DX + L.DY - 1, L.DY, rem);            // smallest k with k*DY >= mlo*DX
+        const int kh = udivmod((mhi + 1) * L.DX + L.DY - 1, L.DY, rem) - 1;  // largest k with k*DY < (mhi+1)*DX
         klo = kl; khi = kh < L.DX - 1 ? kh : L.DX - 1;
     } else {
         klo = mlo; khi = mhi;
@@ -253,7 +270,7 @@ MG_DEV void raster_krange(SM &sm, const LineK &L, int ka, int kb, int y0, uint32
     const int dmaj = L.xmaj ? L.DX : L.DY, dmin = L.xmaj ? L.DY : L.DX;
     const int ax = L.xmaj ? L.sgx : 0, ay = L.xmaj ? 0 : L.sgy;   // per k
     const int bx = L.xmaj ? 0 : L.sgx, by = L.xmaj ? L.sgy : 0;   // per m
-    int m = (ka * dmin) / dmaj, acc = ka * dmin - m * dmaj;
+    int acc, m = udivmod(ka * dmin, dmaj, acc);
     for (int k = ka; k <= kb; k++) {
         band_put(sm, L.x1 + ax * k + bx * m, L.y1 + ay * k + by * m, y0, ord);
         acc += dmin;
@@ -293,10 +310,10 @@ template <class SM>
 MG_DEV void edge_ends(const SM &sm, int k, int &x1, int &y1, int &x2, int &y2, uint32_t &ord, bool &inside) {
     const uint32_t se = sm.sedge[k];
     const int v = se & 0x3FFF, g = sm.v_geom[v];
-    const int nx = (se & 0x4000u) ? v + 1 - sm.g_nv[g] : v + 1;
     const int fd = sm.fdelta[v];
     x1 = sm.vx[v] + (fd & 3) - 1; y1 = sm.vy[v] + ((fd >> 2) & 3) - 1;
-    x2 = sm.vx[nx]; y2 = sm.vy[nx];
+    if (se & 0x4000u) { const int nx = sm.g_voff[g]; x2 = sm.vx[nx]; y2 = sm.vy[nx]; } // closing edge
+    else { x2 = sm.vx[v + 1]; y2 = sm.vy[v + 1]; }
     ord = 2 * g + 2;
     inside = (se & 0x8000u) != 0;
 }
@@ -321,10 +338,11 @@ MG_DEV void item_rows(const SM &sm, int i, int &ylo, int &yhi) {
 // rows of fill edge (ip -> v) under pygame draw_fillpoly's rule: with (ya, xa) the upper end, the
 // edge meets rows ya <= y < yb, plus y == yb when yb is the polygon's last row; horizontal edges none
 template <class SM>
-MG_DEV void fill_edge(const SM &sm, int ve, int &xa, int &ya, int &xb, int &yb, int &side, int &r0, int &r1) {
+MG_DEV void fill_edge(const SM &sm, int ve, int &xa, int &ya, int &xb, int &yb, int &side, int &r0, int &r1,
+                      bool &lastrow) {
     const int v = ve & 0x3FFF, g = sm.v_geom[v];
     const int ip = (ve & 0x4000) ? v + sm.g_nv[g] - 1 : v - 1;
-    const uint4 gi = sm.ginfo[g];
+    const uint2 gi = sm.ginfo[g];
     const int gymin = (int16_t)(gi.x & 0xFFFF), gymax = (int16_t)(gi.x >> 16);
     const bool onscreen = (int16_t)(gi.y & 0xFFFF) <= (int16_t)(gi.y >> 16); // else never in a band list
     int y1 = sm.vy[ip], y2 = sm.vy[v];
@@ -332,7 +350,8 @@ MG_DEV void fill_edge(const SM &sm, int ve, int &xa, int &ya, int &xb, int &yb, 
     if (y1 < y2) { xa = sm.vx[ip]; ya = y1; xb = sm.vx[v]; yb = y2; }
     else { xa = sm.vx[v]; ya = y2; xb = sm.vx[ip]; yb = y1; }
     r0 = ya > 0 ? ya : 0;
-    r1 = yb == gymax ? yb : yb - 1;
+    lastrow = yb == gymax;
+    r1 = lastrow ? yb : yb - 1;
     r1 = r1 < MG_RES - 1 ? r1 : MG_RES - 1;
     if (y1 == y2 || !onscreen) r1 = r0 - 1;
     (void)gymin;
@@ -397,14 +416,14 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         else if (kind == MG_ENT_GOAL) { my_r0 = L->goal_rpoly0; my_nr = L->goal_nrpoly; }
         else if (kind == MG_ENT_ROBOT) { my_r0 = L->robot_rpoly0; my_nr = L->robot_nrpoly; }
         else { int t = AT(S.etype, tid); my_r0 = L->block_rpoly0[t]; my_nr = L->block_nrpoly[t]; }
-        sm.e_g0[tid + 1] = (int16_t)my_nr;
+        sm.u.pre.e_g0[tid + 1] = (int16_t)my_nr;
     }
     if (tid == 0) {
         sm.err = 0; sm.ndash = 0; sm.nsedge = 0; sm.nlong = 0;
         sm.col[0] = pack_rgb(L->background);
-        sm.e_g0[0] = 0;
+        sm.u.pre.e_g0[0] = 0;
     }
-    if (tid < RG_NBANDS) { sm.bin_cnt[tid] = 0; sm.ebin_cnt[tid] = 0; }
+    if (tid < RG_NBANDS) { sm.u.pre.bin_cnt[tid] = 0; sm.u.pre.ebin_cnt[tid] = 0; }
     if (view == 0 && tid == 32) { // Viewer.render: stack.push(self.transform) -> eye(3) @ view
         const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
         mg_mat3_mul(I3, L->allo_view, sm.u.pre.view);
@@ -427,8 +446,8 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         entity_xform(S, e, (tid - 64) / 5, (tid - 64) % 5, sm.u.pre.e_xf[(tid - 64) / 5][(tid - 64) % 5]);
     RG_SYNC();
     if (tid == 0) {
-        for (int k = 0; k < nents; k++) sm.e_g0[k + 1] += sm.e_g0[k];
-        sm.ngeom = sm.e_g0[nents];
+        for (int k = 0; k < nents; k++) sm.u.pre.e_g0[k + 1] += sm.u.pre.e_g0[k];
+        sm.ngeom = sm.u.pre.e_g0[nents];
         if (sm.ngeom > SM::RG_MAXG) sm.err = 2;
     }
     RG_SYNC();
@@ -436,10 +455,10 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     const int G = sm.ngeom;
     if (tid < nents) {
         int ecol = AT(S.ecol, tid);
-        for (int k = 0, g = sm.e_g0[tid]; k < my_nr; k++, g++) {
+        for (int k = 0, g = sm.u.pre.e_g0[tid]; k < my_nr; k++, g++) {
             const mg_rpoly &rp = L->rpoly[my_r0 + k];
-            sm.g_rpoly[g] = (int16_t)(my_r0 + k);
-            sm.g_ent[g] = (int8_t)tid;
+            sm.u.pre.g_rpoly[g] = (int16_t)(my_r0 + k);
+            sm.u.pre.g_ent[g] = (int8_t)tid;
             sm.g_nv[g] = (int16_t)rp.npts;
             sm.col[2 * g + 1] = ref_colour(L, rp.col_ref, ecol);
             sm.col[2 * g + 2] = rp.outline ? ref_colour(L, rp.ocol_ref, ecol) : 0ull;
@@ -449,8 +468,8 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     if (tid < 64) wave_exclusive_scan(sm.g_nv, sm.g_voff, G, lane);
     // ---- 2. per-geom matrix: view @ T_last @ ... @ T_first (Geom.render stack) ----
     for (int g = tid; g < G; g += RG_THREADS) {
-        const mg_rpoly &rp = L->rpoly[sm.g_rpoly[g]];
-        int ent = sm.g_ent[g];
+        const mg_rpoly &rp = L->rpoly[sm.u.pre.g_rpoly[g]];
+        int ent = sm.u.pre.g_ent[g];
         double M[9];
         for (int i = 0; i < 9; i++) M[i] = sm.u.pre.view[i];
         for (int k = rp.nxf - 1; k >= 0; k--) {
@@ -469,9 +488,9 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     // ---- 3. vertices -> int pixel coordinates (pygame (int) truncation); outline edges ----
     for (int v = tid; v < NV; v += RG_THREADS) {
         int g = sm.v_geom[v], i = v - sm.g_voff[g];
-        const mg_rpoly &rp = L->rpoly[sm.g_rpoly[g]];
+        const mg_rpoly &rp = L->rpoly[sm.u.pre.g_rpoly[g]];
         double x, y;
-        rpoly_pt(S, L, e, rp, sm.g_ent[g], i, x, y);
+        rpoly_pt(S, L, e, rp, sm.u.pre.g_ent[g], i, x, y);
         const double *M = sm.u.pre.g_m[g];
         double gx = __fma_rn(M[1], y, M[0] * x) + M[2];
         double gy = __fma_rn(M[4], y, M[3] * x) + M[5];
@@ -481,11 +500,12 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         // lines(): first point via float (pg FloatFromObj), second via int
         sm.fdelta[v] = (uint8_t)(((int)(float)gx - ix + 1) | (((int)(float)gy - iy + 1) << 2));
         if (rp.outline == MG_OUTLINE_SOLID) {
-            sm.sedge[atomicAdd(&sm.nsedge, 1)] = (uint16_t)(v | (i + 1 == rp.npts ? 0x4000 : 0));
+            const int k = atomicAdd(&sm.nsedge, 1);
+            if (k < SM::RG_MAXSEDGE) sm.sedge[k] = (uint16_t)(v | (i + 1 == rp.npts ? 0x4000 : 0));
         } else if (rp.outline == MG_OUTLINE_DASHED) {
             int j = i + 1 == rp.npts ? 0 : i + 1;
             double xb, yb;
-            rpoly_pt(S, L, e, rp, sm.g_ent[g], j, xb, yb);
+            rpoly_pt(S, L, e, rp, sm.u.pre.g_ent[g], j, xb, yb);
             double gxb = __fma_rn(M[1], yb, M[0] * xb) + M[2], gyb = __fma_rn(M[4], yb, M[3] * xb) + M[5];
             push_dashes(sm, gx, gy, gxb, gyb, 2 * g + 2);
         }
@@ -494,14 +514,14 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     // ---- 4. per-geom bounds (vertex-parallel atomics) and the convexity premise of the fill: going
     //         round a polygon the sign of dy changes exactly twice (both vertex chains y-monotone) ----
     for (int g = tid; g < G; g += RG_THREADS) {
-        int32_t *b = (int32_t *)&sm.ginfo[g];
+        int32_t *b = sm.u.pre.gbb[g];
         b[0] = 32767; b[1] = -32768; b[2] = 32767; b[3] = -32768;
-        sm.gchg[g] = 0;
+        sm.u.pre.gchg[g] = 0;
     }
     RG_SYNC();
     for (int v = tid; v < NV; v += RG_THREADS) {
         const int g = sm.v_geom[v], v0 = sm.g_voff[g], n = sm.g_nv[g];
-        int32_t *b = (int32_t *)&sm.ginfo[g];
+        int32_t *b = sm.u.pre.gbb[g];
         const int x = sm.vx[v], y = sm.vy[v];
         atomicMin(&b[0], y); atomicMax(&b[1], y); atomicMin(&b[2], x); atomicMax(&b[3], x);
         const int nx = v + 1 == v0 + n ? v0 : v + 1;
@@ -513,18 +533,19 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             dp = sm.vy[p] - sm.vy[pp];
             p = pp;
         }
-        if ((dp > 0) != (d > 0)) atomicAdd(&sm.gchg[g], 1);
+        if ((dp > 0) != (d > 0)) atomicAdd(&sm.u.pre.gchg[g], 1);
     }
     RG_SYNC();
     for (int g = tid; g < G; g += RG_THREADS) {
-        const int32_t *b = (const int32_t *)&sm.ginfo[g];
+        const int32_t *b = sm.u.pre.gbb[g];
         const int ymin = b[0], ymax = b[1];
         const int xmin = b[2] > 0 ? b[2] : 0, xmax = b[3] < MG_RES - 1 ? b[3] : MG_RES - 1;
-        if (sm.gchg[g] != 2 && sm.gchg[g] != 0) sm.err = 4;
-        sm.ginfo[g] = make_uint4((uint32_t)(uint16_t)ymin | ((uint32_t)(uint16_t)ymax << 16),
-                                 (uint32_t)(uint16_t)xmin | ((uint32_t)(uint16_t)xmax << 16), 0u, 0u);
+        if (sm.u.pre.gchg[g] != 2 && sm.u.pre.gchg[g] != 0) sm.err = 4;
+        sm.ginfo[g] = make_uint2((uint32_t)(uint16_t)ymin | ((uint32_t)(uint16_t)ymax << 16),
+                                 (uint32_t)(uint16_t)xmin | ((uint32_t)(uint16_t)xmax << 16));
     }
     if (sm.ndash > SM::RG_MAXDASH) sm.err = 1;
+    if (sm.nsedge > SM::RG_MAXSEDGE) sm.err = 5;
     const int nitems = sm.nsedge + (sm.ndash < SM::RG_MAXDASH ? sm.ndash : SM::RG_MAXDASH);
     for (int i = tid; i < nitems; i += RG_THREADS) {
         int ylo, yhi;
@@ -538,7 +559,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             if (xl >= 0 && xh + 1 <= MG_RES - 1 && ylo >= 0 && yhi <= MG_RES - 1) sm.sedge[i] |= 0x8000u;
         }
         ylo = ylo > 0 ? ylo : 0; yhi = yhi < MG_RES - 1 ? yhi : MG_RES - 1;
-        for (int b = ylo / RG_BAND; b <= yhi / RG_BAND && ylo <= yhi; b++) atomicAdd(&sm.bin_cnt[b], 1);
+        for (int b = ylo / RG_BAND; b <= yhi / RG_BAND && ylo <= yhi; b++) atomicAdd(&sm.u.pre.bin_cnt[b], 1);
     }
     for (int i = tid; i < SM::RG_MAXG * RG_BAND; i += RG_THREADS)
         (&sm.bspan[0][0])[i] = (uint32_t)RG_EMPTY | ((uint32_t)RG_EMPTY << 16);
@@ -546,18 +567,19 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     for (int v = tid; v < NV; v += RG_THREADS) { // fill edges per band (needs the geoms' row ranges)
         const int ve = v | (v == sm.g_voff[sm.v_geom[v]] ? 0x4000 : 0);
         int xa, ya, xb, yb, side, r0, r1;
-        fill_edge(sm, ve, xa, ya, xb, yb, side, r0, r1);
-        for (int b = r0 / RG_BAND; b <= r1 / RG_BAND && r0 <= r1; b++) atomicAdd(&sm.ebin_cnt[b], 1);
+        bool lastrow;
+        fill_edge(sm, ve, xa, ya, xb, yb, side, r0, r1, lastrow);
+        for (int b = r0 / RG_BAND; b <= r1 / RG_BAND && r0 <= r1; b++) atomicAdd(&sm.u.pre.ebin_cnt[b], 1);
     }
     RG_SYNC();
     if (tid < 64) {
-        wave_exclusive_scan(sm.bin_cnt, sm.bin_off, RG_NBANDS, lane);
-        wave_exclusive_scan(sm.ebin_cnt, sm.ebin_off, RG_NBANDS, lane);
+        wave_exclusive_scan(sm.u.pre.bin_cnt, sm.bin_off, RG_NBANDS, lane);
+        wave_exclusive_scan(sm.u.pre.ebin_cnt, sm.ebin_off, RG_NBANDS, lane);
     }
     RG_SYNC();
     const int nout = sm.bin_off[RG_NBANDS];
     if (nout + sm.ebin_off[RG_NBANDS] > SM::RG_MAXBIN) sm.err = 3;
-    if (tid < RG_NBANDS) { sm.bin_cnt[tid] = sm.bin_off[tid]; sm.ebin_cnt[tid] = nout + sm.ebin_off[tid]; }
+    if (tid < RG_NBANDS) { sm.u.pre.bin_cnt[tid] = sm.bin_off[tid]; sm.u.pre.ebin_cnt[tid] = nout + sm.ebin_off[tid]; }
     RG_SYNC();
     if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
     for (int i = tid; i < nitems; i += RG_THREADS) {
@@ -565,14 +587,15 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         item_rows(sm, i, ylo, yhi);
         ylo = ylo > 0 ? ylo : 0; yhi = yhi < MG_RES - 1 ? yhi : MG_RES - 1;
         for (int b = ylo / RG_BAND; b <= yhi / RG_BAND && ylo <= yhi; b++)
-            sm.bin[atomicAdd(&sm.bin_cnt[b], 1)] = (int16_t)i;
+            sm.bin[atomicAdd(&sm.u.pre.bin_cnt[b], 1)] = (uint16_t)i;
     }
     for (int v = tid; v < NV; v += RG_THREADS) {
         const int ve = v | (v == sm.g_voff[sm.v_geom[v]] ? 0x4000 : 0);
         int xa, ya, xb, yb, side, r0, r1;
-        fill_edge(sm, ve, xa, ya, xb, yb, side, r0, r1);
+        bool lastrow;
+        fill_edge(sm, ve, xa, ya, xb, yb, side, r0, r1, lastrow);
         for (int b = r0 / RG_BAND; b <= r1 / RG_BAND && r0 <= r1; b++)
-            sm.bin[atomicAdd(&sm.ebin_cnt[b], 1)] = (int16_t)ve;
+            sm.bin[atomicAdd(&sm.u.pre.ebin_cnt[b], 1)] = (uint16_t)(ve | (lastrow ? 0x8000 : 0));
     }
     const int nsedge = sm.nsedge;
     MG_PROF(0);
@@ -622,7 +645,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             const int g = base + lane;
             bool ov = false;
             if (g < G) {
-                const uint4 gi = sm.ginfo[g];
+                const uint2 gi = sm.ginfo[g];
                 const int ymin = (int16_t)(gi.x & 0xFFFF), ymax = (int16_t)(gi.x >> 16);
                 const int xmin = (int16_t)(gi.y & 0xFFFF), xmax = (int16_t)(gi.y >> 16);
                 ov = ymax >= y0 && ymin < y0 + RG_BAND && xmin <= xmax;
@@ -637,8 +660,10 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         }
         if (lane == 0) sm.nblist = cnt;
     };
-    // band 0 prologue: outline layer cleared, band list, prefetch (later bands: in the previous band's tail)
+    // band 0 prologue: outline layer cleared (it overlays the setup scratch: after the binning's
+    // counters are done with), band list, prefetch (later bands: in the previous band's tail)
     if (do_pf) prefetch(0);
+    RG_SYNC();
     for (int i = tid; i < RG_BAND * MG_RES / 4; i += RG_THREADS)
         ((uint4 *)&sm.u.post.band[0][0])[i] = make_uint4(0, 0, 0, 0);
     if (tid == 0) sm.nlong = 0;
@@ -658,18 +683,28 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         const bool fwave = tid >= 64 && tid < 128;
         const int lt = tid < 64 ? tid : tid - 64;   // outline-item thread index (waves 0, 2)
         for (int j = sm.ebin_off[band_i] + nout + tid - 64; fwave && j < sm.ebin_off[band_i + 1] + nout && !(dskip & 8); j += 64) {
+            // fill_edge without the geom-bounds lookup: the bin entry carries the closing and last-row flags
             const int ve = sm.bin[j];
-            int xa, ya, xb, yb, side, r0, r1;
-            fill_edge(sm, ve, xa, ya, xb, yb, side, r0, r1);
-            const int slot = sm.gslot[sm.v_geom[ve & 0x3FFF]];
+            const int v = ve & 0x3FFF, g = sm.v_geom[v];
+            const int yv = sm.vy[v], xv = sm.vx[v];
+            int yp, xp;
+            if (ve & 0x4000) { const int ip = v + sm.g_nv[g] - 1; yp = sm.vy[ip]; xp = sm.vx[ip]; }
+            else { yp = sm.vy[v - 1]; xp = sm.vx[v - 1]; }
+            const int side = yp < yv ? 0 : 1;
+            const int xa = side ? xv : xp, ya = side ? yv : yp, xb = side ? xp : xv, yb = side ? yp : yv;
+            const int r0 = ya > 0 ? ya : 0;
+            int r1 = (ve & 0x8000) ? yb : yb - 1;
+            r1 = r1 < MG_RES - 1 ? r1 : MG_RES - 1;
+            const int slot = sm.gslot[g];
             int16_t *col = (int16_t *)&sm.bspan[slot][0] + side;
             const int ra = r0 > y0 ? r0 : y0, rb = r1 < y0 + RG_BAND - 1 ? r1 : y0 + RG_BAND - 1;
             if (ra > rb) continue;
             // x = xa + trunc((y - ya) * (xb - xa) / (yb - ya)), stepped row by row (y >= ya, yb > ya)
             const int d = yb - ya, adx = xb > xa ? xb - xa : xa - xb, sg = xb >= xa ? 1 : -1;
             const int n0 = (ra - ya) * adx;
-            int q = n0 / d, r = n0 - q * d;
-            const int qs = adx / d, rs = adx - qs * d;
+            int r, rs;
+            int q = udivmod(n0, d, r);
+            const int qs = udivmod(adx, d, rs);
             for (int y = ra; y <= rb; y++) {
                 col[2 * (y - y0)] = (int16_t)(xa + sg * q);
                 q += qs; r += rs;
@@ -730,7 +765,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
                 for (int c = 0; c < 4; c++) o[r][c] = 0u;
             for (int slot = 0; slot < ((dskip & 2) ? 0 : nbl); slot++) {
                 const int g = sm.blist[slot];
-                const uint4 gi = sm.ginfo[g];
+                const uint2 gi = sm.ginfo[g];
                 const int xmin = (int16_t)(gi.y & 0xFFFF), xmax = (int16_t)(gi.y >> 16);
                 if (xmax < x0 || xmin > x0 + 3) continue;
                 const uint4 s4 = *(const uint4 *)&sm.bspan[slot][yb];

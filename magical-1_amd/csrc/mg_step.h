@@ -656,7 +656,7 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
     for (int b = 0; b < nb; b++) {
         AT(S.bpx, b) = AT(S.bpx, b) + (AT(S.bvx, b) + AT(S.bvbx, b)) * dt;
         AT(S.bpy, b) = AT(S.bpy, b) + (AT(S.bvy, b) + AT(S.bvby, b)) * dt;
-        body_set_angle(S, e, b, AT(S.ba, b) + (AT(S.bw, b) + AT(S.bwb, b)) * dt);
+        body_set_angle_step(S, e, b, AT(S.ba, b) + (AT(S.bw, b) + AT(S.bwb, b)) * dt);
         AT(S.bvbx, b) = 0.0; AT(S.bvby, b) = 0.0; AT(S.bwb, b) = 0.0;
     }
     int ns = S.nshapes[e];
@@ -1008,7 +1008,7 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
     for (int b = lane; b < nb; b += 64) {
         AT(S.bpx, b) = AT(S.bpx, b) + (AT(S.bvx, b) + AT(S.bvbx, b)) * dt;
         AT(S.bpy, b) = AT(S.bpy, b) + (AT(S.bvy, b) + AT(S.bvby, b)) * dt;
-        body_set_angle(S, e, b, AT(S.ba, b) + (AT(S.bw, b) + AT(S.bwb, b)) * dt);
+        body_set_angle_step(S, e, b, AT(S.ba, b) + (AT(S.bw, b) + AT(S.bwb, b)) * dt);
         AT(S.bvbx, b) = 0.0; AT(S.bvby, b) = 0.0; AT(S.bwb, b) = 0.0;
     }
     __syncthreads();
@@ -1160,7 +1160,7 @@ MG_DEV void robot_set_action(const MGState &S, const mg_library *L, int e, int a
 
 MG_DEV void robot_update(const MGState &S, const mg_library *L, int e) {
     int body = S.robot_body0[e], control = body + 1, cons0 = S.robot_cons0[e];
-    body_set_angle(S, e, control, AT(S.ba, body) + S.rel_turn[e]);
+    AT(S.ba, control) = AT(S.ba, body) + S.rel_turn[e]; // transform unused (body_rot_unused)
     double c = AT(S.brc, body), s = AT(S.brs, body), ts = S.target_speed[e];
     AT(S.bvx, control) = c * 0.0 - s * ts;
     AT(S.bvy, control) = c * ts + s * 0.0;

@@ -113,7 +113,7 @@ class VecMagicalEnv:
             self.obs_ego = torch.empty((n, 96, 96, 3), **u8)
             self.obs_past = torch.empty((n, 96, 96, 12), **u8)
         self.reward = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.done = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.done = torch.zeros(n, dtype=torch.bool, device=dev)  # the C ABI writes u8 0/1: same bytes
         self.eval_score = torch.zeros(n, dtype=torch.float64, device=dev)
         self.target = torch.zeros((n, 4), dtype=torch.float64, device=dev) if self.spec.task == "PickAndPlace" else None
         buf = native.mg_buffers()
@@ -164,7 +164,7 @@ class VecMagicalEnv:
         native.check(self.lib.mg_step(self.handle, ctypes.c_void_p(a.data_ptr()), self._stream()))
         if self.spec.preproc is None:
             self.render_full(out=self.full)
-        return self._obs(), self.reward, self.done.bool(), {"eval_score": self.eval_score}
+        return self._obs(), self.reward, self.done, {"eval_score": self.eval_score}
 
     def random_actions(self, step, key=42, out=None):
         out = out if out is not None else torch.empty(self.num_envs, dtype=torch.uint8, device=self.device)
