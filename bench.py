@@ -12,7 +12,10 @@ training stream does.  Actions come from device Philox (key 42, counter =
 (step, env)).  Multi-GPU: one process per GPU, envs sharded contiguously
 (global env id = rank * envs + i, seed 1000 + id), no data-path collective
 (instances are independent) -> weak scaling; the timed region is bracketed by
-barrier + synchronize and the max over ranks is reported.
+barrier + synchronize and the max over ranks is reported.  --gather adds the north
+star's exchange: each step's results (obs, reward, done, eval_score) of every rank
+all-gathered to every rank as one packed buffer over RCCL, on its own stream,
+overlapping the next step (magical_amd.dist).
 """
 import argparse
 import json
@@ -107,6 +110,9 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--cpu-steps", type=int, default=1500)  # ~16 x 1 s of CPU work (about 15-25 s)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather", action="store_true",
+                    help="N > 1: all-gather every step's packed results (obs, reward, done, score) to every rank "
+                         "(the north star's exchange; magical_amd.dist.ShardedVecEnv), pipelined with the next step")
     ap.add_argument("--no-phase-spread", action="store_true",
                     help="start every env at episode step 0 (resets then happen on the same step for all envs)")
     args = ap.parse_args()
@@ -132,17 +138,32 @@ def main():
         dist.init_process_group("nccl", device_id=device)
     n = args.envs
     seeds = [1000 + rank * n + i for i in range(n)]
-    vec = magical_amd.make_vec(args.env, n, device=str(device), seeds=seeds)
+    gather = args.gather and world > 1
+    if gather:
+        from magical_amd import dist as mdist
+        shard = mdist.ShardedVecEnv(args.env, n, rank=rank, device=str(device), gather=True)
+        vec = shard.vec
+        step = shard.step_async
+    else:
+        vec = magical_amd.make_vec(args.env, n, device=str(device), seeds=seeds)
+        step = vec.step
     lib = vec.lib
     actions = torch.empty(n, dtype=torch.uint8, device=device)
-    vec.reset()
+    if gather:
+        shard.reset_async()
+    else:
+        vec.reset()
     phase_spread = not args.no_phase_spread and spec.max_episode_steps > 1
     if phase_spread:  # env i starts at episode step (global id) mod max_episode_steps
         L = spec.max_episode_steps
         vec.set_episode_steps(torch.tensor([(rank * n + i) % L for i in range(n)], dtype=torch.int32))
     for s in range(args.warmup):
         vec.random_actions(s, out=actions)
-        vec.step(actions)
+        step(actions)
+    if gather:
+        for h in shard.pending:
+            if h is not None:
+                h.wait()
     torch.cuda.synchronize(device)
     native.check(lib.mg_enable_timing(vec.handle, args.steps))
     if world > 1:
@@ -151,7 +172,11 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         vec.random_actions(args.warmup + s, out=actions)
-        vec.step(actions)
+        step(actions)
+    if gather:   # the timed region ends after the last step's gather
+        for h in shard.pending:
+            if h is not None:
+                h.wait()
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -192,7 +217,9 @@ def main():
             "config": {"workload": args.env, "envs_per_gpu": n, "episode_steps": spec.max_episode_steps,
                        "physics_substeps": 10, "solver_iterations": 10, "render": "2 x 384^2 -> 96^2",
                        "phase_spread": phase_spread,
-                       "parallelism": f"dp{world} (envs sharded, no data-path collective)"},
+                       "parallelism": (f"dp{world} (envs sharded; one packed all-gather of every step's results, "
+                                       f"pipelined with the next step)" if gather else
+                                       f"dp{world} (envs sharded, no data-path collective)")},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": pmc, "bytes_per_env_step": per_env, "units_per_launch": n,
@@ -200,10 +227,12 @@ def main():
             "kernel_ms_per_step": {"step_kernel": round(t_step_ms, 4), "reset_kernel": round(t_reset_ms, 4),
                                    "render_kernel": round(t_render_ms, 4), "timed_launches": n_timed},
             "env_errors": errors,
+            "gather": ({"bytes_per_rank_step": shard.layout.nbytes, "ranks": world,
+                        "received_bytes_per_rank_step": (world - 1) * shard.layout.nbytes} if gather else None),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    vec.close()
+    (shard if gather else vec).close()
     if world > 1:
         dist.destroy_process_group()
 

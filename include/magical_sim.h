@@ -95,6 +95,16 @@ int mg_read_timing(mg_sim *sim, double *out);
 /* overwrite every env's episode step counter (BaseEnv.episode_steps, base_env.py:279-283) from device
  * i32[N]: throughput runs stagger episode phases so resets are spread over the timed steps */
 int mg_set_episode_steps(mg_sim *sim, const int32_t *steps_dev, void *stream);
+/* Demo replay through the LoRes observation stages (replaces saved_trajectories.py:63-149,
+ * _MockDemoEnv + preprocess_demos_with_wrapper, for the LoRes preprocessors of
+ * benchmarks/__init__.py:232-307).  frames: device u8[nframes,2,384,384,3] (allo, ego) of one or more
+ * trajectories concatenated, 16-byte aligned; episode_start: device i32[nframes], the index of the
+ * first frame of each frame's trajectory (its reset observation fills the frame stacks);
+ * preproc: 1 LoRes4E (CHW4E/CHW4A: same bytes, channels-first views on the host), 2 LoResStack,
+ * 3 LoRes3EA, 4 LoRes4A; scratch: device u8[nframes,2,96,96,3] workspace; outputs as mg_buffers for
+ * nframes "envs" (out_past NULL for LoResStack).  No mg_sim needed. */
+int mg_replay_lores(const uint8_t *frames, int32_t nframes, const int32_t *episode_start, int32_t preproc,
+                    uint8_t *scratch, uint8_t *out_allo, uint8_t *out_ego, uint8_t *out_past, void *stream);
 void mg_destroy(mg_sim *sim);
 const char *mg_last_error(void);
 

@@ -1,0 +1,128 @@
+// mg_replay.hip -- demo replay through the LoRes observation stages.
+//
+// Replaces saved_trajectories.py:63-149 (_MockDemoEnv replaying stored observations through
+// preprocess_demos_with_wrapper) for the LoRes preprocessors of benchmarks/__init__.py:232-307:
+// FlattenFrameStack / EagerDictFrameStack (:51-147; a trajectory's reset frame fills every stack slot)
+// and cv2.resize(INTER_AREA) to 96^2 (:150-190, the 4x area case: round-half-even of sum / 16).
+// Input: the trajectories' 384^2 (allo, ego) frames, concatenated, already on the device.  Two passes,
+// both HBM-bound byte work: (1) every frame's two views downsampled once into a workspace, (2) each
+// frame's outputs assembled from the workspace frames its stacks reach back to (clamped to the first
+// frame of its trajectory).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "mg_common.h"
+
+namespace {
+constexpr int RES = MG_RES, LO = MG_LORES;
+constexpr size_t LOFR = (size_t)LO * LO * 3;   // bytes of one 96^2 RGB frame
+
+// round-half-even of s / 16 (cv2 resizeAreaFast: saturate_cast<uchar>(sum * (1.f / 16)))
+__device__ __forceinline__ uint32_t area16(uint32_t s) {
+    const uint32_t q = s >> 4, r = s & 15;
+    return q + (r > 8 || (r == 8 && (q & 1)));
+}
+
+// pass 1: one thread per 4 LoRes pixels of one view (16 input pixels per row = 48 B = 3 x 16 B per row)
+__global__ __launch_bounds__(256) void replay_downsample_kernel(const uint8_t *__restrict__ frames, int64_t nviews,
+                                                                uint8_t *__restrict__ lo) {
+    constexpr int QPR = LO / 4;                        // pixel quads per LoRes row
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t fv = gid / (LO * QPR);
+    if (fv >= nviews) return;
+    const int rem = (int)(gid % (LO * QPR)), oy = rem / QPR, q = rem % QPR;
+    const uint8_t *src = frames + (size_t)fv * RES * RES * 3 + ((size_t)(4 * oy) * RES + 16 * q) * 3;
+    uint32_t sum[12];
+#pragma unroll
+    for (int i = 0; i < 12; i++) sum[i] = 0;
+#pragma unroll
+    for (int dy = 0; dy < 4; dy++) {
+        const uint4 *row = (const uint4 *)(src + (size_t)dy * RES * 3);
+        const uint4 a = row[0], b = row[1], c = row[2];
+        const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int k = 0; k < 48; k++) {               // byte k: input pixel k / 3 (-> output k / 12), channel k % 3
+            const uint32_t byte = (w[k / 4] >> (8 * (k % 4))) & 255u;
+            sum[(k / 12) * 3 + k % 3] += byte;
+        }
+    }
+    uint32_t o[3] = {0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 12; i++) o[i / 4] |= area16(sum[i]) << (8 * (i % 4));
+    uint32_t *dst = (uint32_t *)(lo + (size_t)fv * LOFR + ((size_t)oy * LO + 4 * q) * 3);
+    dst[0] = o[0]; dst[1] = o[1]; dst[2] = o[2];
+}
+
+// pass 2: one thread per 4 pixels of one frame.  Stacked outputs concatenate, per pixel, the frames
+// oldest..newest (3 bytes each); src[k] is the workspace frame of stack slot k.
+__device__ __forceinline__ void stack4(const uint8_t *const src[4], size_t pix_off, uint8_t *dst) {
+    uint32_t f[4][3];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int w = 0; w < 3; w++) f[k][w] = ((const uint32_t *)(src[k] + pix_off))[w];
+    uint4 *d = (uint4 *)dst;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        uint32_t o[4];
+#pragma unroll
+        for (int bb = 0; bb < 16; bb++) {  // output byte b: pixel b / 12, slot (b % 12) / 3, channel b % 3
+            const int b = 16 * q + bb, px = b / 12, k = (b % 12) / 3, sb = 3 * px + b % 3;
+            const uint32_t byte = (f[k][sb / 4] >> (8 * (sb % 4))) & 255u;
+            if (bb % 4 == 0) o[bb / 4] = byte; else o[bb / 4] |= byte << (8 * (bb % 4));
+        }
+        d[q] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+__global__ __launch_bounds__(256) void replay_assemble_kernel(const uint8_t *__restrict__ lo,
+                                                              const int32_t *__restrict__ episode_start,
+                                                              int32_t nframes, int32_t preproc, uint8_t *out_allo,
+                                                              uint8_t *out_ego, uint8_t *out_past) {
+    constexpr int Q = LO * LO / 4;
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int f = (int)(gid / Q), q = (int)(gid % Q);
+    if (f >= nframes) return;
+    const int s0 = episode_start[f];
+    const size_t po = (size_t)q * 12;                  // byte offset of this quad in a 96^2 RGB frame
+    auto view = [&](int frame, int v) { return lo + ((size_t)frame * 2 + v) * LOFR; };
+    auto back = [&](int k) { const int g = f - k; return g > s0 ? g : s0; };  // deque filled at reset
+    if (preproc == MG_PREPROC_LORESSTACK) {            // ResizeDictObservation then EagerDictFrameStack(4)
+        for (int v = 0; v < 2; v++) {
+            const uint8_t *src[4] = {view(back(3), v), view(back(2), v), view(back(1), v), view(f, v)};
+            stack4(src, po, (v ? out_ego : out_allo) + (size_t)f * LOFR * 4 + po * 4);
+        }
+        return;
+    }
+    // FlattenFrameStack then resize: allo / ego are the current frames, past_obs the stacks
+    const uint32_t *a32 = (const uint32_t *)(view(f, 0) + po), *g32 = (const uint32_t *)(view(f, 1) + po);
+    uint32_t *oa = (uint32_t *)(out_allo + (size_t)f * LOFR + po), *og = (uint32_t *)(out_ego + (size_t)f * LOFR + po);
+#pragma unroll
+    for (int w = 0; w < 3; w++) { oa[w] = a32[w]; og[w] = g32[w]; }
+    const uint8_t *src[4];
+    if (preproc == MG_PREPROC_LORES4A) {               // allo depth 4, ego depth 0
+        for (int k = 0; k < 4; k++) src[k] = view(back(3 - k), 0);
+    } else if (preproc == MG_PREPROC_LORES3EA) {       // allo depth 1, then ego depth 3
+        src[0] = view(f, 0);
+        for (int k = 1; k < 4; k++) src[k] = view(back(3 - k), 1);
+    } else {                                           // LoRes4E / LoResCHW4E / LoResCHW4A: ego depth 4
+        for (int k = 0; k < 4; k++) src[k] = view(back(3 - k), 1);
+    }
+    stack4(src, po, out_past + (size_t)f * LOFR * 4 + po * 4);
+}
+}  // namespace
+
+// launcher, C linkage (declared in mg_sim.hip next to the ABI entry mg_replay_lores)
+extern "C" hipError_t mg_launch_replay(const uint8_t *frames, int32_t nframes, const int32_t *episode_start,
+                                       int32_t preproc, uint8_t *scratch, uint8_t *out_allo, uint8_t *out_ego,
+                                       uint8_t *out_past, hipStream_t st) {
+    const int64_t nviews = (int64_t)nframes * 2;
+    const int64_t t1 = nviews * LO * (LO / 4);
+    hipLaunchKernelGGL(replay_downsample_kernel, dim3((unsigned)((t1 + 255) / 256)), dim3(256), 0, st, frames, nviews,
+                       scratch);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int64_t t2 = (int64_t)nframes * (LO * LO / 4);
+    hipLaunchKernelGGL(replay_assemble_kernel, dim3((unsigned)((t2 + 255) / 256)), dim3(256), 0, st, scratch,
+                       episode_start, nframes, preproc, out_allo, out_ego, out_past);
+    return hipGetLastError();
+}

@@ -346,6 +346,25 @@ int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
     return rc;
 }
 
+hipError_t mg_launch_replay(const uint8_t *frames, int32_t nframes, const int32_t *episode_start, int32_t preproc,
+                            uint8_t *scratch, uint8_t *out_allo, uint8_t *out_ego, uint8_t *out_past, hipStream_t st);
+
+int mg_replay_lores(const uint8_t *frames, int32_t nframes, const int32_t *episode_start, int32_t preproc,
+                    uint8_t *scratch, uint8_t *out_allo, uint8_t *out_ego, uint8_t *out_past, void *stream) {
+    if (nframes <= 0 || !frames || !episode_start || !scratch || !out_allo || !out_ego)
+        return set_err(-22, "mg_replay_lores: null argument or nframes <= 0");
+    if (preproc != MG_PREPROC_LORES4E && preproc != MG_PREPROC_LORESSTACK && preproc != MG_PREPROC_LORES3EA &&
+        preproc != MG_PREPROC_LORES4A)
+        return set_err(-22, "mg_replay_lores: preproc must be 1 (LoRes4E), 2 (LoResStack), 3 (LoRes3EA) or 4 (LoRes4A)");
+    if (preproc != MG_PREPROC_LORESSTACK && !out_past) return set_err(-22, "mg_replay_lores: out_past required");
+    const void *ptrs[6] = {frames, scratch, out_allo, out_ego, out_past ? out_past : out_allo, episode_start};
+    for (const void *p : ptrs)
+        if (((uintptr_t)p & 15) != 0) return set_err(-22, "mg_replay_lores: buffers must be 16-byte aligned");
+    HIPC(mg_launch_replay(frames, nframes, episode_start, preproc, scratch, out_allo, out_ego, out_past,
+                          as_stream(stream)));
+    return 0;
+}
+
 int mg_render_full(mg_sim *s, uint8_t *out, void *stream) {
     if (!s || !out) return set_err(-22, "mg_render_full: null argument");
     HIPC(hipSetDevice(s->device));

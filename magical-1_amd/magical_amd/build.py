@@ -28,6 +28,7 @@ UNITS = {  # translation unit -> headers it depends on (one unit per kernel fami
     "mg_step_v4.hip": _STEP,
     "mg_step_hbm.hip": _STEP,
     "mg_raster.hip": _PHYS + ["mg_render.h"],
+    "mg_replay.hip": ["mg_common.h"],
 }
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-Wno-unused-result"]
 

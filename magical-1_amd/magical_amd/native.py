@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(HERE, "libmagical_sim_prof.so" if os.environ.get("MAGICA
 
 EXPORTS = ["mg_create", "mg_bind_outputs", "mg_reset", "mg_step", "mg_render_full", "mg_get_bodies",
            "mg_set_body_pose", "mg_get_errors", "mg_seed", "mg_random_actions", "mg_num_envs", "mg_enable_timing", "mg_read_timing",
-           "mg_set_episode_steps", "mg_selftest_sincos", "mg_destroy", "mg_last_error"]
+           "mg_set_episode_steps", "mg_selftest_sincos", "mg_replay_lores", "mg_destroy", "mg_last_error"]
 
 
 class mg_config(ctypes.Structure):
@@ -61,10 +61,14 @@ def load():
     lib.mg_enable_timing.argtypes = [vp, i32]
     lib.mg_read_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
     lib.mg_set_episode_steps.argtypes = [vp, vp, vp]
+    if hasattr(lib, "mg_replay_lores"):   # (a profiling build may predate it; the product library is checked
+        lib.mg_replay_lores.argtypes = [vp, i32, vp, i32, vp, vp, vp, vp, vp]   # by tests/test_host.py)
     lib.mg_destroy.argtypes = [vp]
     lib.mg_destroy.restype = None
     lib.mg_last_error.restype = ctypes.c_char_p
     for name in EXPORTS[:-2]:
+        if not hasattr(lib, name):
+            continue
         if getattr(lib, name).restype is ctypes.c_int:  # default
             getattr(lib, name).restype = i32
     _lib = lib

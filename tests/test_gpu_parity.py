@@ -614,3 +614,41 @@ def test_layout_retry_parity(name, tries, monkeypatch):
             for k in got:
                 assert np.array_equal(got[k][i], ref_i[k]), f"step {t} env {i} obs {k}"
     vec.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["MoveToRegion-Demo-LoRes4E-v0", "MoveToRegion-Demo-LoResCHW4E-v0"])
+def test_packed_gather_pipeline_single_rank(tmp_path, name):
+    """The multi-GPU exchange path on one GPU (a 1-rank RCCL group): the simulator writes each step's
+    outputs straight into views of a packed buffer (bind_outputs), one all_gather_into_tensor per step
+    on a side stream, two buffers alternating; every step's gathered [1, n, ...] views equal a plain
+    VecMagicalEnv run bit for bit (obs, reward, done, eval_score), incl. the CHW views."""
+    import torch.distributed as dist
+    from magical_amd import dist as mdist
+    n, steps = 70, 45
+    dist.init_process_group("nccl", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        shard = mdist.ShardedVecEnv(name, n, rank=0, device="cuda:0", gather=True)
+        ref = magical_amd.make_vec(name, n, seeds=mdist.shard_seeds(n, 0))
+        acts = np.random.RandomState(4).randint(0, 18, (steps, n))
+        got = shard.reset()
+        want = ref.reset()
+        for k in want:
+            assert torch.equal(got[k][0], want[k]), f"reset {k}"
+        handles = []
+        for t in range(steps):
+            a = torch.as_tensor(acts[t], dtype=torch.uint8)
+            handles.append(shard.step_async(a))
+            obs, rew, done, info = ref.step(a)
+            if t >= 1:   # the previous step's gather, read after this step was launched
+                g_obs, g_rew, g_done, g_info = handles[t - 1].results()
+                for k in prev[0]:
+                    assert torch.equal(g_obs[k][0], prev[0][k]), f"step {t - 1} {k}"
+                assert torch.equal(g_rew[0], prev[1]) and torch.equal(g_done[0], prev[2])
+                assert torch.equal(g_info["eval_score"][0], prev[3])
+            prev = ({k: v.clone() for k, v in obs.items()}, rew.clone(), done.clone(), info["eval_score"].clone())
+        shard.close()
+        ref.close()
+    finally:
+        dist.destroy_process_group()

@@ -185,6 +185,103 @@ def test_two_rank_gloo_sharded_rollout_equals_single_process(tmp_path):
     assert np.array_equal(full, ref)
 
 
+PACKED_WORKER = r'''
+import os, sys
+sys.path[:0] = [{root!r} + "/magical-1_amd", {root!r} + "/oracle"]
+import numpy as np, torch, torch.distributed as dist
+import pyoracle as po
+from magical_amd import dist as mdist, registry, envs as mg_envs
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", init_method="env://")
+name = {name!r}
+spec = registry.lookup(name)
+n, steps = 2, 7
+
+class OracleVec:
+    """CPU stand-in for VecMagicalEnv's output binding: the oracle writes each step into the bound views"""
+    device = torch.device("cpu")
+    def __init__(self, seeds):
+        self.envs = [po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, spec.max_episode_steps, seed=s) for s in seeds]
+    def bind_outputs(self, views):
+        self.v = views
+    def _write(self, i, flat, r=0.0, d=False, sc=0.0):
+        off = 0
+        for k, s in mg_envs._obs_shapes(spec).items():
+            m = int(np.prod(s))
+            self.v[k][i].copy_(torch.from_numpy(flat[off:off + m].reshape(self.v[k][i].shape)))
+            off += m
+        self.v["reward"][i] = r; self.v["done"][i] = d; self.v["eval_score"][i] = sc
+    def reset(self):
+        for i, e in enumerate(self.envs):
+            self._write(i, e.reset())
+    def step(self, actions):
+        for i, e in enumerate(self.envs):
+            o, r, d, sc = e.step(int(actions[i]))
+            if d:
+                o = e.reset()
+            self._write(i, o, r, d, sc)
+    def close(self):
+        pass
+
+vec = OracleVec(mdist.shard_seeds(n, rank))
+env = mdist.ShardedVecEnv(name, n, rank=rank, gather=True, vec=vec, device="cpu")
+acts = np.random.RandomState(5).randint(0, 18, (steps, world * n))
+lo, hi = mdist.shard_range(n, rank)
+obs = env.reset()
+handles = []
+for t in range(steps):
+    handles.append(env.step_async(torch.as_tensor(acts[t, lo:hi])))
+obs, rew, done, info = handles[-1].results()
+if rank == 0:
+    np.savez({out!r}, **{{k: v.numpy() for k, v in obs.items()}}, reward=rew.numpy(), done=done.numpy(),
+             score=info["eval_score"].numpy(), nbytes=env.layout.nbytes)
+env.close()
+dist.destroy_process_group()
+'''
+
+
+@pytest.mark.parametrize("name", ["MoveToRegion-Demo-LoRes4E-v0", "ClusterColour-Demo-LoResStack-v0"])
+def test_two_rank_gloo_packed_gather_pipeline(tmp_path, name):
+    """ShardedVecEnv(gather=True) with world_size 2 on CPU tensors: each rank's step outputs are
+    written into views of one packed buffer, one all_gather_into_tensor per step, two buffers
+    alternating (step_async handles of 7 steps kept, the last one read).  The unpacked [W, n, ...]
+    views equal one process running all W * n envs: observations, reward, done, eval_score,
+    across an episode boundary (MoveToRegion: done at 40 is not reached; LoResStack keys)."""
+    out = str(tmp_path / "full.npz")
+    script = tmp_path / "worker.py"
+    script.write_text(PACKED_WORKER.format(root=ROOT, out=out, name=name))
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env))
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    got = np.load(out)
+    import pyoracle as po
+    from magical_amd import envs as mg_envs
+    spec = registry.lookup(name)
+    steps, W, n = 7, 2, 2
+    acts = np.random.RandomState(5).randint(0, 18, (steps, W * n))
+    envs = [po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, spec.max_episode_steps, seed=1000 + i)
+            for i in range(W * n)]
+    for e in envs:
+        e.reset()
+    for t in range(steps):
+        res = [e.step(int(a)) for e, a in zip(envs, acts[t])]
+    shapes = mg_envs._obs_shapes(spec)
+    for i, (o, r, d, sc) in enumerate(res):
+        off = 0
+        for k, s in shapes.items():
+            m = int(np.prod(s))
+            assert np.array_equal(got[k][i // n, i % n], o[off:off + m].reshape(s)), (k, i)
+            off += m
+        assert got["reward"][i // n, i % n] == np.float32(r) and bool(got["done"][i // n, i % n]) == d
+        assert got["score"][i // n, i % n] == sc
+    assert int(got["nbytes"]) % 256 == 0
+
+
 # --------------------------------------------------------------------------- evaluation protocol
 def test_evaluation_protocol_statistics():
     """evaluation.py:13-98: one record per test env of the demo env, mean / t-CI / std (ddof=1),
