@@ -4,7 +4,7 @@
 #include <hip/hip_runtime.h>
 #include "mg_state.h"
 
-struct TaskCfg { int task, flags; };
+struct TaskCfg { int task, flags, coop; };  // coop: one env per 64-lane wave (reset_kernel_coop)
 
 struct RenderOut {
     uint8_t *full;        // [N][2][384][384][3] (full-resolution mode) or null

@@ -170,39 +170,46 @@ MG_DEV void add_block(const MGState &S, const mg_library *L, int e, Builder &B, 
 // A is entity self_ent's shape (or goal); ign = bit mask of entities whose shapes are ignored
 // (pm_randomise_pose ignore_shapes, geom.py:116-264).
 MG_DEV bool query_hits(const MGState &S, const mg_library *L, int e, const ShapeW &A, int self_k, int group, int self_ent,
-                       uint32_t ign, bool self_on) {
+                       uint32_t ign, bool self_on, int lane) {
     if (!self_on) return false; // the queried shape's categories are 0: cpShapeFilterReject for every pair
-    for (int w = 0; w < 4; w++) {
-        ShapeW W;
-        load_wall(w, W);
-        if (!bb_intersects(A, W)) continue;
-        Collision info;
-        collide(A, W, info);
-        if (info.count) return true;
+    // candidates: 4 arena walls, the entities' goal sensors (enabled: categories != 0), the other shapes.
+    // The answer is "any hit", so in a cooperative reset (lane >= 0) lane l tests candidates l, l + 64, ...
+    // and the wave ORs the results; serially (lane < 0) one thread tests them all.
+    const int nents = S.nents[e], ns = S.nshapes[e];
+    const int total = 4 + nents + ns;
+    bool hit = false;
+    for (int c = lane < 0 ? 0 : lane; c < total && !hit; c += lane < 0 ? 1 : 64) {
+        if (c < 4) {
+            ShapeW W;
+            load_wall(c, W);
+            if (!bb_intersects(A, W)) continue;
+            Collision info;
+            collide(A, W, info);
+            hit = info.count != 0;
+        } else if (c < 4 + nents) {
+            const int g = c - 4;
+            if (AT(S.ekind, g) != MG_ENT_GOAL || g == self_ent || ((ign >> g) & 1u) || AT(S.eshape0, g) == 0) continue;
+            ShapeW G;
+            load_goal(AT(S.ex, g), AT(S.ey, g), AT(S.ew, g), AT(S.eh, g), 0, G);
+            if (!bb_intersects(A, G)) continue;
+            Collision info;
+            collide(A, G, info);
+            hit = info.count != 0;
+        } else {
+            const int j = c - 4 - nents;
+            if (j == self_k || !AT(S.scat, j) || ((ign >> AT(S.sent, j)) & 1u)) continue;
+            int gj = AT(S.sgroup, j);
+            if (group != 0 && group == gj) continue;
+            ShapeW O;
+            load_shape(S, L, e, j, 0, O);
+            if (!bb_intersects(A, O)) continue;
+            Collision info;
+            collide(A, O, info);
+            hit = info.count != 0;
+        }
     }
-    const int nents = S.nents[e];
-    for (int g = 0; g < nents; g++) { // goal sensors (enabled: categories != 0)
-        if (AT(S.ekind, g) != MG_ENT_GOAL || g == self_ent || ((ign >> g) & 1u) || AT(S.eshape0, g) == 0) continue;
-        ShapeW G;
-        load_goal(AT(S.ex, g), AT(S.ey, g), AT(S.ew, g), AT(S.eh, g), 0, G);
-        if (!bb_intersects(A, G)) continue;
-        Collision info;
-        collide(A, G, info);
-        if (info.count) return true;
-    }
-    int ns = S.nshapes[e];
-    for (int j = 0; j < ns; j++) {
-        if (j == self_k || !AT(S.scat, j) || ((ign >> AT(S.sent, j)) & 1u)) continue;
-        int gj = AT(S.sgroup, j);
-        if (group != 0 && group == gj) continue;
-        ShapeW O;
-        load_shape(S, L, e, j, 0, O);
-        if (!bb_intersects(A, O)) continue;
-        Collision info;
-        collide(A, O, info);
-        if (info.count) return true;
-    }
-    return false;
+    if (lane >= 0) hit = __ballot(hit) != 0ull;
+    return hit;
 }
 
 MG_DEV int ent_enabled(const MGState &S, int e, int ent) {
@@ -240,24 +247,24 @@ MG_DEV void shift_entity(const MGState &S, int e, int ent, V2 pos, double ang) {
     }
 }
 
-MG_DEV bool entity_collides(const MGState &S, const mg_library *L, int e, int ent, uint32_t ign) {
+MG_DEV bool entity_collides(const MGState &S, const mg_library *L, int e, int ent, uint32_t ign, int lane) {
     if (AT(S.ekind, ent) == MG_ENT_GOAL) {
         ShapeW G;
         load_goal(AT(S.ex, ent), AT(S.ey, ent), AT(S.ew, ent), AT(S.eh, ent), 0, G);
-        return query_hits(S, L, e, G, -1, 0, ent, ign, AT(S.eshape0, ent) != 0);
+        return query_hits(S, L, e, G, -1, 0, ent, ign, AT(S.eshape0, ent) != 0, lane);
     }
     int s0 = AT(S.eshape0, ent), n = AT(S.enshapes, ent);
     for (int k = s0; k < s0 + n; k++) {
         ShapeW A;
         load_shape(S, L, e, k, 0, A);
-        if (query_hits(S, L, e, A, k, AT(S.sgroup, k), ent, ign, AT(S.scat, k) != 0)) return true;
+        if (query_hits(S, L, e, A, k, AT(S.sgroup, k), ent, ign, AT(S.scat, k) != 0, lane)) return true;
     }
     return false;
 }
 
 // pm_randomise_pose (geom.py:116-264); pos_limit / rot_limit < 0 mean None
-MG_DEV int randomise_pose(const MGState &S, const mg_library *L, int e, int ent, bool rand_rot, double pos_limit,
-                          double rot_limit, uint32_t ign = 0u) {
+MG_DEV int randomise_pose(const MGState &S, const mg_library *L, int e, int lane, int ent, bool rand_rot,
+                          double pos_limit, double rot_limit, uint32_t ign = 0u) {
     bool goal = AT(S.ekind, ent) == MG_ENT_GOAL;
     int b0 = goal ? -1 : AT(S.ebody0, ent);
     double orig_a = goal ? 0.0 : AT(S.ba, b0);
@@ -283,7 +290,7 @@ MG_DEV int randomise_pose(const MGState &S, const mg_library *L, int e, int ent,
         double y = mt_uniform(S, e, ylo, yhi);
         double a = rand_rot ? mt_uniform(S, e, rmin, rmax) : orig_a;
         shift_entity(S, e, ent, v2(x, y), a);
-        if (!entity_collides(S, L, e, ent, ign)) return 0;
+        if (!entity_collides(S, L, e, ent, ign, lane)) return 0;
     }
     // PlacementError: every body back to its saved absolute pose (geom.py:250-254: Body.position and
     // Body.angle setters), not a rigid shift relative to the last try
@@ -302,8 +309,8 @@ MG_DEV int randomise_pose(const MGState &S, const mg_library *L, int e, int ent,
     return -1;
 }
 
-MG_DEV void randomise_all(const MGState &S, const mg_library *L, int e, const int *ents, int n, const bool *rand_rot,
-                          double pos_limit, const double *rot_limits, uint32_t ign = 0u) {
+MG_DEV void randomise_all(const MGState &S, const mg_library *L, int e, int lane, const int *ents, int n,
+                          const bool *rand_rot, double pos_limit, const double *rot_limits, uint32_t ign = 0u) {
     for (int retry = 0; retry < 10; retry++) {
         // geom.py:300-319: each entity's filter is captured at the start of every retry and restored when
         // its turn comes, so entities left disabled by a failed retry stay disabled (categories 0)
@@ -315,7 +322,7 @@ MG_DEV void randomise_all(const MGState &S, const mg_library *L, int e, const in
         bool failed = false;
         for (int k = 0; k < n && !failed; k++) {
             ent_set_enabled(S, e, ents[k], (saved >> k) & 1u);
-            if (randomise_pose(S, L, e, ents[k], rand_rot[k], pos_limit, rot_limits[k], ign) != 0) failed = true;
+            if (randomise_pose(S, L, e, lane, ents[k], rand_rot[k], pos_limit, rot_limits[k], ign) != 0) failed = true;
         }
         if (!failed) return;
     }
@@ -415,6 +422,9 @@ __constant__ static const int FC_REGION_COLOURS[3] = {MG_COL_GREEN, MG_COL_GREEN
 
 MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg) {
     size_t N = (size_t)S.N;
+    // cooperative reset (reset_kernel_coop): the wave's 64 lanes all run this env's reset with the same
+    // values; the shape queries of the rejection samplers are split across them (query_hits)
+    const int lane = cfg.coop ? (int)(threadIdx.x & 63) : -1;
     const int f = cfg.flags;
     S.episode_steps[e] = 0;
     for (int i = 0; i < MG_MAX_ARB; i++) { AT(S.akey, i) = -1; AT(S.acount, i) = 0; AT(S.astate, i) = ARB_FIRST; }
@@ -441,7 +451,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             rl[0] = -1; rl[1] = minor ? JITTER_ROT_BOUND : -1;
             n = 2;
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
-            randomise_all(S, L, e, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl);
+            randomise_all(S, L, e, lane, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl);
         }
     } else if (cfg.task == MG_TASK_MOVE_TO_CORNER) {
         double rx = mt_double(S, e), ry = mt_double(S, e);
@@ -453,7 +463,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
         if (minor) {
             ents[0] = 1; ents[1] = 2; rr[0] = rr[1] = true; rl[0] = rl[1] = JITTER_ROT_BOUND; n = 2;
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
-            randomise_all(S, L, e, ents, n, rr, JITTER_POS_BOUND, rl);
+            randomise_all(S, L, e, lane, ents, n, rr, JITTER_POS_BOUND, rl);
         }
     } else if (cfg.task == MG_TASK_CLUSTER_COLOUR || cfg.task == MG_TASK_CLUSTER_SHAPE) {
         int by = cfg.task == MG_TASK_CLUSTER_SHAPE ? 1 : 0;
@@ -483,7 +493,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             n = nblk + 1;
             for (int i = 0; i < n; i++) { rr[i] = true; rl[i] = full ? -1.0 : JITTER_ROT_BOUND; }
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
-            randomise_all(S, L, e, ents, n, rr, full ? -1.0 : JITTER_POS_BOUND, rl);
+            randomise_all(S, L, e, lane, ents, n, rr, full ? -1.0 : JITTER_POS_BOUND, rl);
         }
     } else if (cfg.task == MG_TASK_MAKE_LINE) { // make_line.py:86-132
         int nblk = 4;
@@ -504,7 +514,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             n = nblk + 1;
             for (int i = 0; i < n; i++) { rr[i] = true; rl[i] = minor ? JITTER_ROT_BOUND : -1.0; }
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
-            randomise_all(S, L, e, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl);
+            randomise_all(S, L, e, lane, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl);
         }
     } else if (cfg.task == MG_TASK_FIND_DUPE) { // find_dupe.py:62-199
         int qcol = MG_COL_YELLOW, qtype = MG_SHAPE_PENTAGON, cols[6], types[6];
@@ -538,13 +548,13 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             for (int i = 0; i < n_out; i++) ents[n++] = 2 + i;
             for (int i = 0; i < n; i++) { rr[i] = i != 0; rl[i] = minor ? JITTER_ROT_BOUND : -1.0; }
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
-            randomise_all(S, L, e, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl, 1u << query);
+            randomise_all(S, L, e, lane, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl, 1u << query);
             if (!(S.overflow[e] & 2)) { // the query block last, mostly inside the placed sensor
                 double lim = fmin(th, tw) / 2 - L->robot_radius * 0.6 / 2;
                 lim = lim > 0 ? lim : 0.0;
                 if (minor) lim = fmin(JITTER_POS_BOUND, lim);
                 shift_entity(S, e, query, v2(AT(S.ex, 1), AT(S.ey, 1)), AT(S.ba, AT(S.ebody0, query)));
-                if (randomise_pose(S, L, e, query, true, lim, minor ? JITTER_ROT_BOUND : -1.0, 1u << 1) != 0)
+                if (randomise_pose(S, L, e, lane, query, true, lim, minor ? JITTER_ROT_BOUND : -1.0, 1u << 1) != 0)
                     S.overflow[e] |= 2;
             }
         }
@@ -587,7 +597,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             ents[n++] = S.nents[e] - 1;
             for (int i = 0; i < n; i++) { rr[i] = i == nr; rl[i] = minor ? JITTER_ROT_BOUND : -1.0; }
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
-            randomise_all(S, L, e, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl, blocks);
+            randomise_all(S, L, e, lane, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl, blocks);
             if (!(S.overflow[e] & 2)) {
                 for (int i = 0; i < nr; i++) {
                     const int b = 1 + nr + i;
@@ -597,7 +607,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
                     double lim = fmin(rh[i], rw[i]) / 2 - L->robot_radius * 0.6;
                     lim = lim > 0 ? lim : 0.0;
                     if (minor) lim = fmin(JITTER_POS_BOUND, lim);
-                    if (randomise_pose(S, L, e, 1 + nr + i, true, lim, minor ? JITTER_ROT_BOUND : -1.0, 1u << (1 + i)) != 0) {
+                    if (randomise_pose(S, L, e, lane, 1 + nr + i, true, lim, minor ? JITTER_ROT_BOUND : -1.0, 1u << (1 + i)) != 0) {
                         S.overflow[e] |= 2;
                         break;
                     }
@@ -629,7 +639,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             n = 4;
             for (int i = 0; i < 4; i++) { ents[i] = 1 + i; rr[i] = true; rl[i] = -1.0; }
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
-            randomise_all(S, L, e, ents, n, rr, -1.0, rl);
+            randomise_all(S, L, e, lane, ents, n, rr, -1.0, rl);
         }
         if (S.target_out) {
             double *t = S.target_out + 4 * (size_t)e;
@@ -680,7 +690,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             for (int i = 0; i < nblk; i++) ents[n++] = first + i;
             for (int i = 0; i < n; i++) { rr[i] = i != 0; rl[i] = minor ? JITTER_ROT_BOUND : -1.0; }
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
-            randomise_all(S, L, e, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl);
+            randomise_all(S, L, e, lane, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl);
         }
     }
     S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;

@@ -7,11 +7,13 @@ __global__ void __launch_bounds__(64) seed_kernel(MGState S, const uint32_t *__r
     mt_seed(S, e, seeds[e]);
 }
 
+// one env per 64-lane wave: the serial reset runs on every lane (identical values, identical stores),
+// the rejection samplers' shape queries are split across the lanes (query_hits)
 __global__ void __launch_bounds__(64) reset_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg,
-                                                   const uint8_t *__restrict__ mask) {
-    int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= S.n_envs) return;
-    if (mask && !mask[e]) return;
+                                                        const uint8_t *__restrict__ mask) {
+    const int e = blockIdx.x;
+    if (e >= S.n_envs || (mask && !mask[e])) return;
+    cfg.coop = 1;
     reset_env(S, L, e, cfg);
 }
 
@@ -23,7 +25,7 @@ hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream
 }
 
 hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, const uint8_t *mask, hipStream_t st) {
-    hipLaunchKernelGGL(reset_kernel, dim3(grid64(S)), dim3(64), 0, st, S, L, cfg, mask);
+    hipLaunchKernelGGL(reset_kernel, dim3(S.n_envs), dim3(64), 0, st, S, L, cfg, mask);
     return hipGetLastError();
 }
 

@@ -4,6 +4,6 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out/cfg
 export PYTHONDONTWRITEBYTECODE=1
 for spec in "MoveToRegion-Demo-LoRes4E-v0 4096" "MoveToCorner-Demo-LoRes4E-v0 4096" "ClusterColour-Demo-LoResStack-v0 8192" "MatchRegions-TestAll-LoRes4E-v0 8192"; do
   set -- $spec
-  timeout -k 10 300 python bench.py --env $1 --envs $2 --steps 30 --warmup 5 --no-cpu-baseline > gpurun_out/cfg/$1.log 2>&1 || { echo "FAIL $1"; tail -5 gpurun_out/cfg/$1.log; exit 1; }
+  timeout -k 10 300 python bench.py --env $1 --envs $2 --steps 60 --warmup 10 --no-cpu-baseline > gpurun_out/cfg/$1.log 2>&1 || { echo "FAIL $1"; tail -5 gpurun_out/cfg/$1.log; exit 1; }
   python -c "import json,sys; d=json.loads(open('gpurun_out/cfg/$1.log').read().strip().splitlines()[-1]); print('$1', $2, d['value'], d['kernel_ms_per_step'], 'errors', d['env_errors'])"
 done
