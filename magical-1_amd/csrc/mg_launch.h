@@ -20,7 +20,7 @@ struct RenderOut {
 hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream_t st);
 hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, const uint8_t *mask, hipStream_t st);
 // LDS-resident substeps: per-env slot caps of a task and envs per workgroup
-struct StepCaps { int nb, ns, nc, na, blk; };
+struct StepCaps { int nb, ns, nc, na, blk, shw; };  // shw: world-space shape scratch per lane in LDS
 size_t mg_step_lds_bytes(const StepCaps &c, int blk);
 // compiled LDS variant matching these caps for n_envs (0: the HBM-state kernel)
 int mg_step_variant(const StepCaps &c, int n_envs);
@@ -29,11 +29,11 @@ bool mg_step_blk_ok(int variant, int blk);
 // Slot caps of the LDS-resident variants (compile-time, so every LDS address folds to a constant
 // offset from the lane's column): 0 = state stays in HBM.
 __host__ __device__ constexpr StepCaps step_variant_caps(int v) {
-    return v == 1 ? StepCaps{6, 5, 10, 20, 16}    // robot only (MoveToRegion)
-         : v == 2 ? StepCaps{7, 6, 12, 32, 16}    // robot + one single-shape block (MoveToCorner)
-         : v == 3 ? StepCaps{14, 53, 26, 48, 1}   // up to 8 blocks incl. stars (Cluster*, MatchRegions): runtime lists
-         : v == 4 ? StepCaps{14, 53, 26, 48, 1}   // the same scenes, one env per 64-lane wavefront (cooperative)
-         : StepCaps{0, 0, 0, 0, 0};
+    return v == 1 ? StepCaps{6, 5, 10, 20, 16, 3}    // robot only (MoveToRegion)
+         : v == 2 ? StepCaps{7, 6, 12, 32, 16, 0}    // robot + one single-shape block (MoveToCorner; no LDS left for shapes)
+         : v == 3 ? StepCaps{14, 53, 26, 48, 1, 0}   // up to 8 blocks incl. stars (Cluster*, MatchRegions): runtime lists
+         : v == 4 ? StepCaps{14, 53, 26, 48, 1, 0}   // the same scenes, one env per 64-lane wavefront (cooperative)
+         : StepCaps{0, 0, 0, 0, 0, 0};
 }
 
 // one compiled step-kernel form (defined in mg_stepk.h, instantiated in mg_step_*.hip)

@@ -216,28 +216,39 @@ MG_DEV Closest closest_points_new(const MinkP &v0, const MinkP &v1) {
     return {pa, pb, vmult(p, 1.0 / (d2 + DBL_MIN)), d2};
 }
 
+// EPA's polytope holds support-point ids (ia << 8 | ib) and rebuilds each Minkowski point from the two
+// shapes when it is read: the same operands, so the same bits as storing the points (a 4-byte entry
+// instead of a 56-byte one keeps the per-lane scratch small)
+MG_DEV V2 shape_point(const ShapeW &sh, int idx) {
+    return sh.type == WS_CIRCLE ? sh.c : sh.type == WS_SEGMENT ? (idx ? sh.b : sh.a) : sh.v[idx];
+}
+MG_DEV MinkP mink(const ShapeW &s1, const ShapeW &s2, uint32_t id) {
+    const V2 pa = shape_point(s1, (int)((id >> 8) & 0xFF)), pb = shape_point(s2, (int)(id & 0xFF));
+    return {pa, pb, vsub(pb, pa), id};
+}
+
 #define MG_EPA_MAX 40
 MG_DEV Closest epa(const ShapeW &s1, const ShapeW &s2, MinkP v0, MinkP v1, MinkP v2_) {
-    MinkP hull[MG_EPA_MAX], hull2[MG_EPA_MAX];
+    uint32_t hull[MG_EPA_MAX], hull2[MG_EPA_MAX];
     int count = 3;
-    hull[0] = v0; hull[1] = v1; hull[2] = v2_;
+    hull[0] = v0.id; hull[1] = v1.id; hull[2] = v2_.id;
     for (int iteration = 1;; iteration++) {
         int mini = 0;
         double minDist = INFINITY;
         for (int j = 0, i = count - 1; j < count; i = j, j++) {
-            double d = closest_dist(hull[i].ab, hull[j].ab);
+            double d = closest_dist(mink(s1, s2, hull[i]).ab, mink(s1, s2, hull[j]).ab);
             if (d < minDist) { minDist = d; mini = i; }
         }
-        MinkP w0 = hull[mini], w1 = hull[(mini + 1) % count];
+        MinkP w0 = mink(s1, s2, hull[mini]), w1 = mink(s1, s2, hull[(mini + 1) % count]);
         MinkP p = support(s1, s2, vperp(vsub(w1.ab, w0.ab)));
         bool duplicate = (p.id == w0.id || p.id == w1.id);
         if (!duplicate && check_area(w1.ab, p.ab) && iteration < 30 && count < MG_EPA_MAX - 1) {
             int count2 = 1;
-            hull2[0] = p;
+            hull2[0] = p.id;
             for (int i = 0; i < count; i++) {
                 int index = (mini + 1 + i) % count;
-                V2 h0 = hull2[count2 - 1].ab, h1 = hull[index].ab;
-                V2 h2 = (i + 1 < count ? hull[(index + 1) % count] : p).ab;
+                V2 h0 = mink(s1, s2, hull2[count2 - 1]).ab, h1 = mink(s1, s2, hull[index]).ab;
+                V2 h2 = (i + 1 < count ? mink(s1, s2, hull[(index + 1) % count]) : p).ab;
                 if (check_area(vsub(h2, h0), vadd(vsub(h1, h0), vsub(h1, h2)))) hull2[count2++] = hull[index];
             }
             for (int i = 0; i < count2; i++) hull[i] = hull2[i];

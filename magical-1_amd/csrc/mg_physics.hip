@@ -2,6 +2,7 @@
 // 1/2: compile-time constraint lists, 3/4: LDS views with runtime lists, 0: HBM state) and envs per
 // workgroup.  The forms themselves live in mg_step_*.hip (one translation unit each).
 #include "mg_launch.h"
+#include "mg_phys.h"   // sizeof(ShapeW) of the LDS views
 
 // LDS bytes of one env's view (same carve order as carve_view, per-lane columns)
 size_t mg_step_lds_bytes(const StepCaps &c, int blk) {
@@ -19,6 +20,7 @@ size_t mg_step_lds_bytes(const StepCaps &c, int blk) {
     take(SH, 2); take(SH, 2); take(SH, 1); take(SH, 1);
     for (int i = 0; i < 3; i++) take(C, 1);
     for (int i = 0; i < 5; i++) take(A, 1);
+    take((size_t)c.shw * blk, sizeof(ShapeW));
     return (off + 15) & ~(size_t)15;
 }
 

@@ -191,9 +191,9 @@ static int pick_step_variant(const StepCaps &c, int n_envs, int task) {
     int v = mg_step_variant(c, n_envs);
     if (v == 3) v = 4;
     const char *ov = getenv("MG_STEP_VARIANT");
-    if (ov) { // experiments: 0 (HBM state), the scene's compiled variant, or 3 <-> 4 (LDS runtime lists)
+    if (ov) { // experiments: 0 (HBM state), the scene's compiled variant, 3 / 4 (LDS runtime lists)
         const int w = atoi(ov), base = mg_step_variant(c, n_envs);
-        if (w == 0 || w == base || (base == 3 && w == 4)) v = w;
+        if (w == 0 || w == base || w == 3 || w == 4) v = w;   // 3 / 4 fit every scene (caps 14/53/26/48)
     }
     return v;
 }
@@ -260,6 +260,7 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     s->S.cons_cap = MG_MAX_CONS;
     s->S.arb_cap = MG_MAX_ARB;
     s->S.max_tries = 10000; // geom.py:198
+    s->S.shw = nullptr;     // HBM-state kernels keep their narrowphase shapes in registers / scratch
     if (const char *mt = getenv("MG_DEBUG_MAX_TRIES")) s->S.max_tries = atoi(mt) > 0 ? atoi(mt) : 10000; // tests only
     s->S.N = (cfg->num_envs + 63) / 64 * 64;
     Carver sizing = {nullptr, 0};

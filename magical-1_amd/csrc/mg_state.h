@@ -9,6 +9,8 @@
 #pragma once
 #include "mg_common.h"
 
+struct ShapeW;  // mg_phys.h
+
 struct MGState {
     int N;      // padded env count (multiple of 64); row stride of every [slot][N] array
     int n_envs; // live env count
@@ -63,6 +65,9 @@ struct MGState {
     uint8_t *hist_allo;      // [4][N][96*96*3]
     uint8_t *hist_ego;       // [4][N][96*96*3]
     int32_t *hist_head;      // [N] ring head
+    // LDS views of the compile-time robot scenes: 3 world-space shapes per lane (narrowphase operands:
+    // the queried shape, a wall, the other shape) in LDS instead of per-lane scratch; null elsewhere
+    ShapeW *shw;
 };
 
 // constraint parameter slots (cp[k][c][env])

@@ -663,10 +663,15 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
     for (int k = 0; k < ns; k++) shape_update_bb(S, L, e, k);
     MG_PP(P, 1);
     // broadphase + narrowphase, canonical order
+    // narrowphase operands: in the LDS view's per-lane shape scratch for the compile-time scenes (LDS
+    // latency instead of per-lane scratch memory), locals elsewhere
+    ShapeW locA, locW, locB;
+    constexpr bool LDS_SHAPES = NCS > 0 && step_variant_caps(NCS == 10 ? 1 : 2).shw > 0;
+    ShapeW &A = LDS_SHAPES ? S.shw[3 * e] : locA, &W = LDS_SHAPES ? S.shw[3 * e + 1] : locW;
+    ShapeW &B = LDS_SHAPES ? S.shw[3 * e + 2] : locB;
     for (int i = 0; i < ns; i++) {
         // BB tests on the cached BBs; the world-space shape is built only for pairs that pass
         const double al = AT(S.sbbl, i), ab = AT(S.sbbb, i), ar = AT(S.sbbr, i), at = AT(S.sbbt, i);
-        ShapeW A;
         bool have_a = false;
         const int gi = AT(S.sgroup, i), bi = AT(S.sbody, i);
         const double ui = AT(S.su, i);
@@ -675,7 +680,6 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
             wall_bb(w, wl, wb, wr, wt);
             if (!(al <= wr && wl <= ar && ab <= wt && wb <= at)) continue;
             if (!have_a) { load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A); have_a = true; }
-            ShapeW W;
             load_wall(w, W);
             Collision info;
             collide(A, W, info);
@@ -688,7 +692,6 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
             int gj = AT(S.sgroup, j);
             if ((gi != 0 && gi == gj) || ((gi | gj) & MG_GROUP_OFF)) continue; // cpShapeFilterReject
             if (!have_a) { load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A); have_a = true; }
-            ShapeW B;
             load_shape(S, L, e, j, (uint64_t)AT(S.shash, j), B);
             Collision info;
             collide(A, B, info);

@@ -47,6 +47,7 @@ __device__ __forceinline__ void carve_view(MGState &V, unsigned char *smem, cons
     V.ctype = carve<int8_t>(smem, off, C); V.ca = carve<int8_t>(smem, off, C); V.cb = carve<int8_t>(smem, off, C);
     V.astate = carve<int8_t>(smem, off, A); V.acount = carve<int8_t>(smem, off, A); V.asa = carve<int8_t>(smem, off, A);
     V.asb = carve<int8_t>(smem, off, A); V.active = carve<int8_t>(smem, off, A);
+    V.shw = c.shw ? carve<ShapeW>(smem, off, (size_t)c.shw * blk) : nullptr;
     V.N = blk;
     V.cons_cap = c.nc;
     V.arb_cap = c.na;
