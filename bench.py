@@ -87,17 +87,18 @@ def cpu_baseline(name, workers, steps):
 
 
 def load_pmc(kernel, workload, envs):
-    """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/pmc_traffic.json),
-    only when they were collected on this workload and env count."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        data = json.load(f)
-    rec = data.get(kernel)
-    if not rec or rec.get("workload") != workload or rec.get("envs") != envs:
-        return None
-    return rec["bytes_per_launch"]
+    """PMC record of `kernel` (HBM bytes per launch, VALU issue fraction) from the committed passes:
+    profiles/pmc_traffic.json, else profiles/r02_table/<workload>.traffic.json (tools/gpu_table.sh), only
+    when they were collected on this workload and env count."""
+    for path in (os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                 os.path.join(ROOT, "profiles", "r02_table", f"{workload}.traffic.json")):
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            rec = json.load(f).get(kernel)
+        if rec and rec.get("workload") == workload and rec.get("envs") == envs:
+            return rec
+    return None
 
 
 def main():
@@ -222,8 +223,12 @@ def main():
                                        f"dp{world} (envs sharded, no data-path collective)")},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": pmc, "bytes_per_env_step": per_env, "units_per_launch": n,
-                         "kernel_avg_ms": round(dom_ms, 4)},
+                         "traffic": pmc and pmc["bytes_per_launch"], "bytes_per_env_step": per_env,
+                         "units_per_launch": n, "kernel_avg_ms": round(dom_ms, 4),
+                         # the binding resource is VALU issue, not HBM: SQ_INSTS_VALU x 2 cycles over
+                         # 1024 SIMDs x GRBM_GUI_ACTIVE / 8 of the committed SQ pass (profiles/)
+                         "valu_issue_frac": pmc and pmc.get("valu_issue_frac"),
+                         "wait_any_frac": pmc and pmc.get("wait_any_frac")},
             "kernel_ms_per_step": {"step_kernel": round(t_step_ms, 4), "reset_kernel": round(t_reset_ms, 4),
                                    "render_kernel": round(t_render_ms, 4), "timed_launches": n_timed},
             "env_errors": errors,

@@ -445,6 +445,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     if (tid >= 64 && tid - 64 < 5 * nents)
         entity_xform(S, e, (tid - 64) / 5, (tid - 64) % 5, sm.u.pre.e_xf[(tid - 64) / 5][(tid - 64) % 5]);
     RG_SYNC();
+    MG_PROF(10);
     if (tid == 0) {
         for (int k = 0; k < nents; k++) sm.u.pre.e_g0[k + 1] += sm.u.pre.e_g0[k];
         sm.ngeom = sm.u.pre.e_g0[nents];
@@ -466,6 +467,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     }
     RG_SYNC();
     if (tid < 64) wave_exclusive_scan(sm.g_nv, sm.g_voff, G, lane);
+    MG_PROF(11);
     // ---- 2. per-geom matrix: view @ T_last @ ... @ T_first (Geom.render stack) ----
     for (int g = tid; g < G; g += RG_THREADS) {
         const mg_rpoly &rp = L->rpoly[sm.u.pre.g_rpoly[g]];
@@ -485,6 +487,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     for (int g = tid; g < G; g += RG_THREADS)
         for (int i = 0, v0 = sm.g_voff[g]; i < sm.g_nv[g]; i++) sm.v_geom[v0 + i] = (uint8_t)g;
     RG_SYNC();
+    MG_PROF(12);
     // ---- 3. vertices -> int pixel coordinates (pygame (int) truncation); outline edges ----
     for (int v = tid; v < NV; v += RG_THREADS) {
         int g = sm.v_geom[v], i = v - sm.g_voff[g];
@@ -511,6 +514,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         }
     }
     RG_SYNC();
+    MG_PROF(13);
     // ---- 4. per-geom bounds (vertex-parallel atomics) and the convexity premise of the fill: going
     //         round a polygon the sign of dy changes exactly twice (both vertex chains y-monotone) ----
     for (int g = tid; g < G; g += RG_THREADS) {
@@ -564,6 +568,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     for (int i = tid; i < SM::RG_MAXG * RG_BAND; i += RG_THREADS)
         (&sm.bspan[0][0])[i] = (uint32_t)RG_EMPTY | ((uint32_t)RG_EMPTY << 16);
     RG_SYNC();
+    MG_PROF(14);
     for (int v = tid; v < NV; v += RG_THREADS) { // fill edges per band (needs the geoms' row ranges)
         const int ve = v | (v == sm.g_voff[sm.v_geom[v]] ? 0x4000 : 0);
         int xa, ya, xb, yb, side, r0, r1;
@@ -582,6 +587,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     if (tid < RG_NBANDS) { sm.u.pre.bin_cnt[tid] = sm.bin_off[tid]; sm.u.pre.ebin_cnt[tid] = nout + sm.ebin_off[tid]; }
     RG_SYNC();
     if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
+    MG_PROF(15);
     for (int i = tid; i < nitems; i += RG_THREADS) {
         int ylo, yhi;
         item_rows(sm, i, ylo, yhi);

@@ -37,14 +37,17 @@ for s in range(steps):
 torch.cuda.synchronize()
 lib.mg_debug_read_profile(buf)
 v = list(buf)
-R = ["setup(1-5)", "band clear+prefetch", "band lines", "band fill+resolve", "band output"]
+R = ["setup: bin fill", "band clear+prefetch", "band lines", "band fill+resolve", "band output"]
 X = ["max-thread lines work", "max-thread fill work", "long segments", "bin items", "band geoms"]
 P = ["robot_update", "integrate+bb", "broad+narrow", "arb filter", "prestep", "cached impulses", "iterations",
      "tail(score/reset)"]
 for view, base in (("allo", 0), ("ego", 16)):
-    tot = sum(v[base:base + 5])
+    tot = sum(v[base:base + 5]) + sum(v[base + 10:base + 16])
     print(f"render {view}: total {tot / 1e6:.1f}M ticks over {steps} steps x {n} WGs")
     for i, nm in enumerate(R):
+        print(f"   {nm:22s} {v[base + i] / max(tot, 1) * 100:6.1f}%  {v[base + i] / (steps * n):10.0f} ticks/WG")
+    for i, nm in zip(range(10, 16), ["  setup: ents/xforms", "  setup: geom tables", "  setup: matrices",
+                                      "  setup: verts+dashes", "  setup: bounds+count", "  setup: ebin count+scan"]):
         print(f"   {nm:22s} {v[base + i] / max(tot, 1) * 100:6.1f}%  {v[base + i] / (steps * n):10.0f} ticks/WG")
     for i, nm in enumerate(X):
         print(f"   {nm:22s} {v[base + 5 + i] / (steps * n):10.1f} per WG (sum over bands)")
