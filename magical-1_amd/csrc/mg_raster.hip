@@ -3,10 +3,24 @@
 #include "mg_render.h"
 
 hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderOut &ro, int mode, hipStream_t st) {
-    if (ro.small)
-        hipLaunchKernelGGL(render_kernel<RenderSmem<RG_SMALL>>, dim3(S.n_envs, 2), dim3(RG_THREADS), 0, st, S, L, ro, mode);
-    else
-        hipLaunchKernelGGL(render_kernel<RenderSmem<RG_LARGE>>, dim3(S.n_envs, 2), dim3(RG_THREADS), 0, st, S, L, ro, mode);
+    const dim3 grid(S.n_envs, 2), blk(RG_THREADS);
+    RenderOut r = ro;
+    if (ro.small) {   // the small class holds every MoveToRegion / MoveToCorner scene
+        r.retry_mode = 0;
+        if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_SMALL>, 0>), grid, blk, 0, st, S, L, r);
+        else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_SMALL>, 1>), grid, blk, 0, st, S, L, r);
+        return hipGetLastError();
+    }
+    // the medium class (twice the workgroups per CU of the large one) holds typical scenes of the
+    // many-block tasks; the (env, view) pairs it cannot hold are marked and rendered by the large class
+    r.retry_mode = 1;
+    if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM>, 0>), grid, blk, 0, st, S, L, r);
+    else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM>, 1>), grid, blk, 0, st, S, L, r);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    r.retry_mode = 2;
+    if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_LARGE>, 0>), grid, blk, 0, st, S, L, r);
+    else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_LARGE>, 1>), grid, blk, 0, st, S, L, r);
     return hipGetLastError();
 }
 

@@ -21,10 +21,12 @@
 #include "mg_prof.h"
 
 // capacity classes (template parameters of the LDS layout): geoms, vertices, dash lines, bin entries
-// (outline items + fill edges, binned per band), solid outline edges.  The large class fits every task; the small one fits
-// robot + arena + goal + one block (MoveToRegion / MoveToCorner) and leaves room for 5 workgroups/CU.
-#define RG_LARGE 160, 1600, 256, 3072, 1600
-#define RG_SMALL 32, 704, 160, 1536, 256
+// (outline items + fill edges, binned per band), solid outline edges, entities, outline-mask type (one bit
+// per entity).  The large class fits every task; the small one fits robot + arena + goal + one block
+// (MoveToRegion / MoveToCorner) and leaves room for 9 workgroups/CU.
+#define RG_LARGE 160, 1600, 256, 3072, 1600, MG_MAX_ENTS, uint32_t
+#define RG_MEDIUM 64, 1024, 256, 2048, 768, MG_MAX_ENTS, uint32_t
+#define RG_SMALL 32, 704, 160, 1536, 256, 6, uint8_t
 #define RG_MAXLONG 16
 #define RG_BAND 8
 #define RG_NBANDS (MG_RES / RG_BAND)
@@ -56,26 +58,35 @@ MG_DEV int udivmod(int n, int d, int &r) {
 struct LineK { int x1, y1, sgx, sgy, DX, DY, xmaj; };
 
 // LDS: the setup matrices / scratch and the band buffers are never live at the same time, so they
-// share storage.  Small class: 6 workgroups per CU (<= 26 KiB); large class: 3.
-template <int MAXG_, int MAXVERT_, int MAXDASH_, int MAXBIN_, int MAXSEDGE_>
+// share storage.  Small class: 9 workgroups per CU (< 17 KiB); large class: 3.
+//
+// Outline layer, MT = u32: the largest outline ordinal drawn at each pixel (atomicMax).  MT = u8: every
+// entity draws at most one outlined polygon (the library builder checks it), and entities are drawn in
+// add order, so "largest outline ordinal at a pixel" is "highest entity bit set at the pixel": the
+// layer holds one bit per entity (atomicOr on words of 4 pixels) and oord[] maps the entity back to its
+// outline's ordinal -- a quarter of the LDS.
+template <int MAXG_, int MAXVERT_, int MAXDASH_, int MAXBIN_, int MAXSEDGE_, int MAXE_, typename MT_>
 struct RenderSmem {
     static constexpr int RG_MAXG = MAXG_, RG_MAXVERT = MAXVERT_, RG_MAXDASH = MAXDASH_, RG_MAXBIN = MAXBIN_,
-                         RG_MAXSEDGE = MAXSEDGE_;
+                         RG_MAXSEDGE = MAXSEDGE_, RG_MAXE = MAXE_;
+    static constexpr int MBITS = 8 * (int)sizeof(MT_), MPW = 4 / (int)sizeof(MT_);   // bits / pixels per word
+    static constexpr uint32_t MMASK = (1u << MBITS) - 1u;
+    static constexpr bool ORDMAX = MBITS == 32;                                      // layer of ordinals
+    static_assert(ORDMAX || (MAXE_ <= MBITS && MAXE_ <= MG_MAX_ENTS), "one outline-mask bit per entity");
     union alignas(16) {
         struct {
             double g_m[RG_MAXG][6];
-            double e_xf[MG_MAX_ENTS][5][9];
+            double e_xf[RG_MAXE][5][9];
             double view[9];
             // setup scratch (dead before the bands)
             int32_t gbb[RG_MAXG][4];                 // per-geom ymin, ymax, xmin, xmax while built (atomics)
             int32_t gchg[RG_MAXG];                   // direction changes of the y sequence around each polygon
             int32_t bin_cnt[RG_NBANDS], ebin_cnt[RG_NBANDS];
             int16_t g_rpoly[RG_MAXG];
-            int8_t g_ent[RG_MAXG];
-            int16_t e_g0[MG_MAX_ENTS + 1];
+            int16_t e_g0[RG_MAXE + 1];
         } pre;
         struct {
-            uint32_t band[RG_BAND][MG_RES]; // outline layer of the current band
+            uint32_t band[RG_BAND][MG_RES / MPW]; // outline layer of the current band (entity bits per pixel)
             uint4 lo[RG_BANDLO16];          // current frame, 2 LoRes rows
             int32_t lk[RG_MAXLONG][7];      // long segments of this band (LineK)
             int32_t lkr[RG_MAXLONG][3];     // klo, khi, ordinal
@@ -91,7 +102,9 @@ struct RenderSmem {
     uint16_t sedge[RG_MAXSEDGE];              // solid outline edges: start vertex | last << 14 | inside << 15
     int16_t blist[RG_MAXG];                   // geoms overlapping the current band, in draw order
     int16_t dash[RG_MAXDASH][4];              // clipped dashed-outline lines
-    int16_t dash_o[RG_MAXDASH];
+    uint16_t dash_o[RG_MAXDASH];              // outline-layer value of each dash line
+    int8_t g_ent[RG_MAXG];
+    uint16_t oord1[17];                       // [k + 1]: ordinal of entity k's outlined polygon (0: none)
     int16_t bin_off[RG_NBANDS + 1];           // per-band outline item lists (in bin[])
     int16_t ebin_off[RG_NBANDS + 1];          // per-band fill edge lists (in bin[], after the outline items)
     uint16_t bin[RG_MAXBIN];                  // outline item index, or fill edge: vertex | closing << 14 | last-row << 15
@@ -175,7 +188,7 @@ MG_DEV void push_line(SM &sm, int x1, int y1, int x2, int y2, int ord) {
     int i = atomicAdd(&sm.ndash, 1);
     if (i >= SM::RG_MAXDASH) { sm.err = 1; return; }
     sm.dash[i][0] = (int16_t)x1; sm.dash[i][1] = (int16_t)y1; sm.dash[i][2] = (int16_t)x2; sm.dash[i][3] = (int16_t)y2;
-    sm.dash_o[i] = (int16_t)ord;
+    sm.dash_o[i] = (uint16_t)ord;
 }
 
 // clip_and_draw_line_width (pygame 1.9.6): base line + offsets 1, -1, 2, ...
@@ -232,9 +245,12 @@ MG_DEV void push_dashes(SM &sm, double x1, double y1, double x2, double y2, int 
 }
 
 template <class SM>
-MG_DEV void band_put(SM &sm, int x, int y, int y0, uint32_t ord) {
+MG_DEV void band_put(SM &sm, int x, int y, int y0, uint32_t obit) {
     int r = y - y0;
-    if (r >= 0 && r < RG_BAND && x >= 0 && x < MG_RES) atomicMax(&sm.u.post.band[r][x], ord);
+    if (r >= 0 && r < RG_BAND && x >= 0 && x < MG_RES) {
+        if constexpr (SM::ORDMAX) atomicMax(&sm.u.post.band[r][x], obit);
+        else atomicOr(&sm.u.post.band[r][x / SM::MPW], obit << (SM::MBITS * (x % SM::MPW)));
+    }
 }
 
 // pygame drawline of a clipped segment in k-form (major axis has |d|+1 pixels,
@@ -314,7 +330,7 @@ MG_DEV void edge_ends(const SM &sm, int k, int &x1, int &y1, int &x2, int &y2, u
     x1 = sm.vx[v] + (fd & 3) - 1; y1 = sm.vy[v] + ((fd >> 2) & 3) - 1;
     if (se & 0x4000u) { const int nx = sm.g_voff[g]; x2 = sm.vx[nx]; y2 = sm.vy[nx]; } // closing edge
     else { x2 = sm.vx[v + 1]; y2 = sm.vy[v + 1]; }
-    ord = 2 * g + 2;
+    ord = SM::ORDMAX ? 2 * g + 2 : 1u << sm.g_ent[g];   // the outline layer's value
     inside = (se & 0x8000u) != 0;
 }
 
@@ -400,14 +416,20 @@ MG_DEV void entity_xform(const MGState &S, int e, int ent, int x, double *xf) {
 }
 
 // One (env, view) per workgroup.  mode 0: LoRes outputs; mode 1: full-resolution frames.
-template <class SM>
-__global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out,
-                                                            int mode) {
+template <class SM, int MODE>
+__global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     __shared__ SM sm;
+    constexpr int mode = MODE;
     const int e = blockIdx.x, view = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
     if (e >= S.n_envs || (out.mask && !out.mask[e])) return;
+    if (out.retry_mode == 2 && !S.rg_retry[2 * e + view]) return;
     MG_PROF_BEGIN(tid == 0);
+    // capacity overflow: the medium class hands the (env, view) to the large class, else an env error
+#define RG_FAIL() do { \
+        if (tid == 0) { if (out.retry_mode == 1) S.rg_retry[2 * e + view] = 1; else S.overflow[e] |= 4 << view; } \
+        return; } while (0)
     const int nents = S.nents[e];
+    if (nents > SM::RG_MAXE || (out.retry_mode == 1 && out.force_retry)) RG_FAIL();
     // ---- 1. geometry list (entity add order x render polys), colour table, view ----
     int my_r0 = 0, my_nr = 0;
     if (tid < nents) {
@@ -424,6 +446,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         sm.u.pre.e_g0[0] = 0;
     }
     if (tid < RG_NBANDS) { sm.u.pre.bin_cnt[tid] = 0; sm.u.pre.ebin_cnt[tid] = 0; }
+    if (tid < 17) sm.oord1[tid] = 0;
     if (view == 0 && tid == 32) { // Viewer.render: stack.push(self.transform) -> eye(3) @ view
         const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
         mg_mat3_mul(I3, L->allo_view, sm.u.pre.view);
@@ -446,20 +469,25 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         entity_xform(S, e, (tid - 64) / 5, (tid - 64) % 5, sm.u.pre.e_xf[(tid - 64) / 5][(tid - 64) % 5]);
     RG_SYNC();
     MG_PROF(10);
+    if (out.retry_mode == 2 && tid == 0) S.rg_retry[2 * e + view] = 0;   // every wave has read it (barrier above)
     if (tid == 0) {
         for (int k = 0; k < nents; k++) sm.u.pre.e_g0[k + 1] += sm.u.pre.e_g0[k];
         sm.ngeom = sm.u.pre.e_g0[nents];
         if (sm.ngeom > SM::RG_MAXG) sm.err = 2;
     }
     RG_SYNC();
-    if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
+    if (sm.err) RG_FAIL();
     const int G = sm.ngeom;
     if (tid < nents) {
         int ecol = AT(S.ecol, tid);
         for (int k = 0, g = sm.u.pre.e_g0[tid]; k < my_nr; k++, g++) {
             const mg_rpoly &rp = L->rpoly[my_r0 + k];
             sm.u.pre.g_rpoly[g] = (int16_t)(my_r0 + k);
-            sm.u.pre.g_ent[g] = (int8_t)tid;
+            sm.g_ent[g] = (int8_t)tid;
+            if (rp.outline) {
+                if (sm.oord1[tid + 1]) sm.err = 6;   // two outlined polygons in one entity: the mask needs one
+                sm.oord1[tid + 1] = (uint16_t)(2 * g + 2);
+            }
             sm.g_nv[g] = (int16_t)rp.npts;
             sm.col[2 * g + 1] = ref_colour(L, rp.col_ref, ecol);
             sm.col[2 * g + 2] = rp.outline ? ref_colour(L, rp.ocol_ref, ecol) : 0ull;
@@ -471,7 +499,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     // ---- 2. per-geom matrix: view @ T_last @ ... @ T_first (Geom.render stack) ----
     for (int g = tid; g < G; g += RG_THREADS) {
         const mg_rpoly &rp = L->rpoly[sm.u.pre.g_rpoly[g]];
-        int ent = sm.u.pre.g_ent[g];
+        int ent = sm.g_ent[g];
         double M[9];
         for (int i = 0; i < 9; i++) M[i] = sm.u.pre.view[i];
         for (int k = rp.nxf - 1; k >= 0; k--) {
@@ -483,7 +511,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     }
     RG_SYNC();
     const int NV = sm.g_voff[G];
-    if (NV > SM::RG_MAXVERT) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
+    if (NV > SM::RG_MAXVERT) RG_FAIL();
     for (int g = tid; g < G; g += RG_THREADS)
         for (int i = 0, v0 = sm.g_voff[g]; i < sm.g_nv[g]; i++) sm.v_geom[v0 + i] = (uint8_t)g;
     RG_SYNC();
@@ -493,7 +521,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         int g = sm.v_geom[v], i = v - sm.g_voff[g];
         const mg_rpoly &rp = L->rpoly[sm.u.pre.g_rpoly[g]];
         double x, y;
-        rpoly_pt(S, L, e, rp, sm.u.pre.g_ent[g], i, x, y);
+        rpoly_pt(S, L, e, rp, sm.g_ent[g], i, x, y);
         const double *M = sm.u.pre.g_m[g];
         double gx = __fma_rn(M[1], y, M[0] * x) + M[2];
         double gy = __fma_rn(M[4], y, M[3] * x) + M[5];
@@ -508,9 +536,9 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         } else if (rp.outline == MG_OUTLINE_DASHED) {
             int j = i + 1 == rp.npts ? 0 : i + 1;
             double xb, yb;
-            rpoly_pt(S, L, e, rp, sm.u.pre.g_ent[g], j, xb, yb);
+            rpoly_pt(S, L, e, rp, sm.g_ent[g], j, xb, yb);
             double gxb = __fma_rn(M[1], yb, M[0] * xb) + M[2], gyb = __fma_rn(M[4], yb, M[3] * xb) + M[5];
-            push_dashes(sm, gx, gy, gxb, gyb, 2 * g + 2);
+            push_dashes(sm, gx, gy, gxb, gyb, SM::ORDMAX ? 2 * g + 2 : 1 << sm.g_ent[g]);
         }
     }
     RG_SYNC();
@@ -586,7 +614,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     if (nout + sm.ebin_off[RG_NBANDS] > SM::RG_MAXBIN) sm.err = 3;
     if (tid < RG_NBANDS) { sm.u.pre.bin_cnt[tid] = sm.bin_off[tid]; sm.u.pre.ebin_cnt[tid] = nout + sm.ebin_off[tid]; }
     RG_SYNC();
-    if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; return; }
+    if (sm.err) RG_FAIL();
     MG_PROF(15);
     for (int i = tid; i < nitems; i += RG_THREADS) {
         int ylo, yhi;
@@ -670,7 +698,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     // counters are done with), band list, prefetch (later bands: in the previous band's tail)
     if (do_pf) prefetch(0);
     RG_SYNC();
-    for (int i = tid; i < RG_BAND * MG_RES / 4; i += RG_THREADS)
+    for (int i = tid; i < (int)(sizeof(sm.u.post.band) / 16); i += RG_THREADS)
         ((uint4 *)&sm.u.post.band[0][0])[i] = make_uint4(0, 0, 0, 0);
     if (tid == 0) sm.nlong = 0;
     if (tid >= 128) band_list(0);
@@ -791,11 +819,24 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             uint64_t sum = 0;
 #pragma unroll
             for (int r = 0; r < ((dskip & 32) ? 0 : 4); r++) {
-                const uint4 lv = *(const uint4 *)&sm.u.post.band[yb + r][x0];
-                o[r][0] = o[r][0] > lv.x ? o[r][0] : lv.x;
-                o[r][1] = o[r][1] > lv.y ? o[r][1] : lv.y;
-                o[r][2] = o[r][2] > lv.z ? o[r][2] : lv.z;
-                o[r][3] = o[r][3] > lv.w ? o[r][3] : lv.w;
+                if constexpr (SM::ORDMAX) {
+                    const uint4 lv = *(const uint4 *)&sm.u.post.band[yb + r][x0];
+                    o[r][0] = o[r][0] > lv.x ? o[r][0] : lv.x;
+                    o[r][1] = o[r][1] > lv.y ? o[r][1] : lv.y;
+                    o[r][2] = o[r][2] > lv.z ? o[r][2] : lv.z;
+                    o[r][3] = o[r][3] > lv.w ? o[r][3] : lv.w;
+                } else {
+                    // the highest entity bit of each pixel -> that entity's outline ordinal (oord1[0] = 0)
+                    const uint32_t w = sm.u.post.band[yb + r][ox];
+                    if (w) {
+#pragma unroll
+                        for (int c = 0; c < 4; c++) {
+                            const uint32_t m = (w >> (8 * c)) & 255u;
+                            const uint32_t oo = sm.oord1[m ? 32 - __clz((int)m) : 0];
+                            o[r][c] = o[r][c] > oo ? o[r][c] : oo;
+                        }
+                    }
+                }
 #pragma unroll
                 for (int c = 0; c < 4; c++) sum += sm.col[o[r][c]];
             }
@@ -827,7 +868,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         // next band's empty spans, cleared outline layer, band list (wave 2) and prefetch
         for (int i = tid; i < nbl * RG_BAND; i += RG_THREADS)
             (&sm.bspan[0][0])[i] = (uint32_t)RG_EMPTY | ((uint32_t)RG_EMPTY << 16);
-        for (int i = tid; i < ((dskip & 128) ? 0 : RG_BAND * MG_RES / 4); i += RG_THREADS)
+        for (int i = tid; i < ((dskip & 128) ? 0 : (int)(sizeof(sm.u.post.band) / 16)); i += RG_THREADS)
             ((uint4 *)&sm.u.post.band[0][0])[i] = make_uint4(0, 0, 0, 0);
         if (tid == 0) sm.nlong = 0;
         if (mode == 0 && !(dskip & 4)) {
@@ -878,3 +919,4 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     if (mode == 0 && tid == 0) S.hist_head[view * S.N + e] = nh;
     MG_PROF_END(16 * view);
 }
+#undef RG_FAIL

@@ -29,6 +29,7 @@ static int set_err(int code, const std::string &msg) {
 
 struct mg_sim {
     MGState S;
+    int force_render_retry;   // tests: the medium render class hands every (env, view) to the large class
     mg_library *dlib;
     void *pool;
     size_t pool_bytes;
@@ -135,6 +136,7 @@ static void layout(MGState &S, Carver &c) {
     S.acon = c.take<double>((size_t)2 * AC_NUM * A); S.ahash = c.take<uint64_t>(2 * A);
     S.active = c.take<int8_t>(A); S.nactive = c.take<int32_t>(N); S.stamp = c.take<uint32_t>(N);
     S.curr_dt = c.take<double>(N); S.overflow = c.take<int32_t>(N);
+    S.rg_retry = c.take<uint8_t>(2 * N);
     S.target_speed = c.take<double>(N); S.rel_turn = c.take<double>(N); S.target_finger = c.take<double>(N);
     S.robot_body0 = c.take<int32_t>(N); S.robot_cons0 = c.take<int32_t>(N); S.pv = c.take<double>(5 * N);
     S.ekind = c.take<int8_t>(E); S.etype = c.take<int8_t>(E); S.ecol = c.take<int8_t>(E); S.erole = c.take<int8_t>(E);
@@ -208,11 +210,12 @@ static int pick_step_blk(int variant) {
 static int grid64(const mg_sim *s) { return (s->S.n_envs + 63) / 64; }
 
 static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
-    RenderOut ro;
+    RenderOut ro = {};
     ro.full = nullptr;
     ro.mask = mask;
     ro.debug_skip = 0;
     ro.small = s->task == MG_TASK_MOVE_TO_REGION || s->task == MG_TASK_MOVE_TO_CORNER;
+    ro.force_retry = s->force_render_retry;
 #ifdef MG_PROFILE
     if (getenv("MG_DEBUG_SKIP")) ro.debug_skip = atoi(getenv("MG_DEBUG_SKIP"));
 #endif
@@ -262,6 +265,7 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     s->S.max_tries = 10000; // geom.py:198
     s->S.shw = nullptr;     // HBM-state kernels keep their narrowphase shapes in registers / scratch
     if (const char *mt = getenv("MG_DEBUG_MAX_TRIES")) s->S.max_tries = atoi(mt) > 0 ? atoi(mt) : 10000; // tests only
+    s->force_render_retry = getenv("MG_DEBUG_RENDER_RETRY") != nullptr;                                     // tests only
     s->S.N = (cfg->num_envs + 63) / 64 * 64;
     Carver sizing = {nullptr, 0};
     layout(s->S, sizing);
@@ -374,6 +378,7 @@ int mg_render_full(mg_sim *s, uint8_t *out, void *stream) {
     ro.full = out;
     ro.preproc = s->preproc;
     ro.small = s->task == MG_TASK_MOVE_TO_REGION || s->task == MG_TASK_MOVE_TO_CORNER;
+    ro.force_retry = s->force_render_retry;
     HIPC(mg_launch_render(s->S, s->dlib, ro, 1, as_stream(stream)));
     return 0;
 }

@@ -609,6 +609,11 @@ def build_library():
             add_r(pts, outline, col, ocol, [XF_MAIN])
         L.block_nrpoly[t] = len(rpolys) - L.block_rpoly0[t]
     assert len(rpolys) <= MAX_RPOLYS and len(rpts) <= MAX_RPTS
+    # the render kernel's outline layer holds one bit per entity (mg_render.h RenderSmem): at most one
+    # outlined polygon per entity kind
+    for r0, n in ([(L.arena_rpoly0, L.arena_nrpoly), (L.goal_rpoly0, L.goal_nrpoly), (L.robot_rpoly0, L.robot_nrpoly)]
+                  + [(L.block_rpoly0[t], L.block_nrpoly[t]) for t in range(NUM_SHAPE_TYPES)]):
+        assert sum(1 for i in range(r0, r0 + n) if rpolys[i][2] != OUTLINE_NONE) <= 1
     L.n_rpolys = len(rpolys)
     for i, (npts, off, outline, col, ocol, xfs) in enumerate(rpolys):
         rp = L.rpoly[i]

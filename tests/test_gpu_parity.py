@@ -114,7 +114,7 @@ def test_rollout_parity(name, n, steps):
     vec.close()
 
 
-# every compiled step-kernel form, forced through the experiment switches read at mg_create
+# every compiled step-kernel (and render-class) form, forced through the experiment switches read at mg_create
 # (MG_STEP_VARIANT: 0 = HBM state, 1/2 = compile-time constraint lists, 3 = LDS with runtime lists and
 # one env per single-lane workgroup, 4 (default for those scenes) = the same one env per 64-lane wavefront;
 # MG_STEP_BLK / MG_STEP_BLK0: envs per workgroup)
@@ -132,6 +132,9 @@ KERNEL_FORMS = [
     ("ClusterShape-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0"}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0"}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "8"}),
+    # render classes of the many-block tasks: the medium class hands every (env, view) to the large one
+    ("ClusterColour-TestAll-LoResStack-v0", 66, 30, {"MG_DEBUG_RENDER_RETRY": "1"}),
+    ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_DEBUG_RENDER_RETRY": "1"}),
 ]
 
 
@@ -304,8 +307,10 @@ def test_scores_with_placed_blocks(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", [c[0] for c in CONFIGS])
-def test_full_resolution_frames(name):
+@pytest.mark.parametrize("name,retry", [(c[0], False) for c in CONFIGS] + [("MatchRegions-TestAll-LoRes4E-v0", True)])
+def test_full_resolution_frames(name, retry, monkeypatch):
+    if retry:   # the large render class, through the medium class's hand-over
+        monkeypatch.setenv("MG_DEBUG_RENDER_RETRY", "1")
     spec = registry.lookup(name)
     n = 3
     seeds = [7 + i for i in range(n)]
