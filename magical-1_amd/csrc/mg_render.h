@@ -25,7 +25,7 @@
 // per entity).  The large class fits every task; the small one fits robot + arena + goal + one block
 // (MoveToRegion / MoveToCorner) and leaves room for 9 workgroups/CU.
 #define RG_LARGE 160, 1600, 256, 3072, 1600, MG_MAX_ENTS, uint32_t
-#define RG_MEDIUM 64, 1024, 256, 2048, 768, MG_MAX_ENTS, uint32_t
+#define RG_MEDIUM 64, 1024, 256, 2048, 768, MG_MAX_ENTS, uint16_t
 #define RG_SMALL 32, 704, 160, 1536, 256, 6, uint8_t
 #define RG_MAXLONG 16
 #define RG_BAND 8
@@ -76,7 +76,7 @@ struct RenderSmem {
     union alignas(16) {
         struct {
             double g_m[RG_MAXG][6];
-            double e_xf[RG_MAXE][5][9];
+            double e_xf[RG_MAXE + 4][9];   // main transform per entity, then the robot's 4 others (xf_slot)
             double view[9];
             // setup scratch (dead before the bands)
             int32_t gbb[RG_MAXG][4];                 // per-geom ymin, ymax, xmin, xmax while built (atomics)
@@ -415,6 +415,10 @@ MG_DEV void entity_xform(const MGState &S, int e, int ent, int x, double *xf) {
     }
 }
 
+// LDS slot of entity ent's transform x: the main transforms by entity, the robot's fingers and pupils after
+template <class SM>
+MG_DEV int xf_slot(int ent, int x) { return x == MG_XF_MAIN ? ent : SM::RG_MAXE + x - 1; }
+
 // One (env, view) per workgroup.  mode 0: LoRes outputs; mode 1: full-resolution frames.
 template <class SM, int MODE>
 __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
@@ -465,8 +469,11 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
         mg_mat3_mul(I3, m1, sm.u.pre.view);
     }
-    if (tid >= 64 && tid - 64 < 5 * nents)
-        entity_xform(S, e, (tid - 64) / 5, (tid - 64) % 5, sm.u.pre.e_xf[(tid - 64) / 5][(tid - 64) % 5]);
+    if (tid >= 64 && tid - 64 < 5 * nents) {
+        const int ent = (tid - 64) / 5, x = (tid - 64) % 5;
+        if (x == MG_XF_MAIN || AT(S.ekind, ent) == MG_ENT_ROBOT)   // one robot per scene
+            entity_xform(S, e, ent, x, sm.u.pre.e_xf[xf_slot<SM>(ent, x)]);
+    }
     RG_SYNC();
     MG_PROF(10);
     if (out.retry_mode == 2 && tid == 0) S.rg_retry[2 * e + view] = 0;   // every wave has read it (barrier above)
@@ -504,7 +511,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         for (int i = 0; i < 9; i++) M[i] = sm.u.pre.view[i];
         for (int k = rp.nxf - 1; k >= 0; k--) {
             int x = rp.xf[k];
-            const double *T = x >= MG_XF_STATIC0 ? L->static_xf[x - MG_XF_STATIC0] : sm.u.pre.e_xf[ent][x];
+            const double *T = x >= MG_XF_STATIC0 ? L->static_xf[x - MG_XF_STATIC0] : sm.u.pre.e_xf[xf_slot<SM>(ent, x)];
             mg_mat3_mul(M, T, M);
         }
         for (int i = 0; i < 6; i++) sm.u.pre.g_m[g][i] = M[i];
@@ -827,11 +834,14 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
                     o[r][3] = o[r][3] > lv.w ? o[r][3] : lv.w;
                 } else {
                     // the highest entity bit of each pixel -> that entity's outline ordinal (oord1[0] = 0)
-                    const uint32_t w = sm.u.post.band[yb + r][ox];
-                    if (w) {
+                    uint32_t w0, w1;
+                    if constexpr (SM::MPW == 4) { w0 = sm.u.post.band[yb + r][ox]; w1 = 0u; }
+                    else { const uint2 t = *(const uint2 *)&sm.u.post.band[yb + r][2 * ox]; w0 = t.x; w1 = t.y; }
+                    if (w0 | w1) {
 #pragma unroll
                         for (int c = 0; c < 4; c++) {
-                            const uint32_t m = (w >> (8 * c)) & 255u;
+                            const uint32_t wc = (SM::MPW == 4 || c < 2) ? w0 : w1;
+                            const uint32_t m = (wc >> (SM::MBITS * (c % SM::MPW))) & SM::MMASK;
                             const uint32_t oo = sm.oord1[m ? 32 - __clz((int)m) : 0];
                             o[r][c] = o[r][c] > oo ? o[r][c] : oo;
                         }
