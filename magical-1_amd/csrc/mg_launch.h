@@ -15,8 +15,10 @@ struct RenderOut {
     int preproc;
     int debug_skip;       // profiling builds only: 1 skip outlines, 2 skip fill, 4 skip HBM stores, 8 skip spans
     int small;            // 1: robot + arena + goal + one block at most (MoveToRegion, MoveToCorner) -> small LDS class
-    int retry_mode;       // set by mg_launch_render: 1 medium class (marks S.rg_retry), 2 large class (renders the marked)
-    int force_retry;      // tests: the medium class marks every (env, view)
+    int retry_in;         // set by mg_launch_render: render only the (env, view) pairs marked in S.rg_retry
+    int retry_out;        // ... a pair this class cannot hold is marked for the next class (else an env error)
+    int cls_level;        // ... position of this class in the chain
+    int force_retry;      // tests: classes below this level mark every pair (1: skip the first, 2: the first two)
 };
 
 hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream_t st);

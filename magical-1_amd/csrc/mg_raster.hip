@@ -5,20 +5,27 @@
 hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderOut &ro, int mode, hipStream_t st) {
     const dim3 grid(S.n_envs, 2), blk(RG_THREADS);
     RenderOut r = ro;
+    r.retry_in = r.retry_out = r.cls_level = 0;
     if (ro.small) {   // the small class holds every MoveToRegion / MoveToCorner scene
-        r.retry_mode = 0;
         if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_SMALL>, 0>), grid, blk, 0, st, S, L, r);
         else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_SMALL>, 1>), grid, blk, 0, st, S, L, r);
         return hipGetLastError();
     }
-    // the medium class (twice the workgroups per CU of the large one) holds typical scenes of the
-    // many-block tasks; the (env, view) pairs it cannot hold are marked and rendered by the large class
-    r.retry_mode = 1;
-    if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM>, 0>), grid, blk, 0, st, S, L, r);
-    else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM>, 1>), grid, blk, 0, st, S, L, r);
+    // many-block tasks: a chain of classes, each with more LDS (fewer workgroups per CU) than the last;
+    // the (env, view) pairs a class cannot hold are marked and rendered by the next one (the others exit
+    // at once).  Medium-1 (7 workgroups/CU) holds most scenes of the benchmark tasks, medium-2 (5) nearly
+    // all, the large class (3) every scene.
+    r.retry_out = 1;
+    if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM1>, 0>), grid, blk, 0, st, S, L, r);
+    else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM1>, 1>), grid, blk, 0, st, S, L, r);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    r.retry_mode = 2;
+    r.retry_in = 1; r.cls_level = 1;
+    if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM2>, 0>), grid, blk, 0, st, S, L, r);
+    else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM2>, 1>), grid, blk, 0, st, S, L, r);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    r.retry_out = 0; r.cls_level = 2;
     if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_LARGE>, 0>), grid, blk, 0, st, S, L, r);
     else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_LARGE>, 1>), grid, blk, 0, st, S, L, r);
     return hipGetLastError();

@@ -25,7 +25,8 @@
 // per entity).  The large class fits every task; the small one fits robot + arena + goal + one block
 // (MoveToRegion / MoveToCorner) and leaves room for 9 workgroups/CU.
 #define RG_LARGE 160, 1600, 256, 3072, 1600, MG_MAX_ENTS, uint32_t
-#define RG_MEDIUM 64, 1024, 256, 2048, 768, MG_MAX_ENTS, uint16_t
+#define RG_MEDIUM1 48, 896, 160, 1536, 512, MG_MAX_ENTS, uint16_t
+#define RG_MEDIUM2 96, 1280, 160, 2560, 768, MG_MAX_ENTS, uint16_t
 #define RG_SMALL 32, 704, 160, 1536, 256, 6, uint8_t
 #define RG_MAXLONG 16
 #define RG_BAND 8
@@ -426,14 +427,14 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     constexpr int mode = MODE;
     const int e = blockIdx.x, view = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
     if (e >= S.n_envs || (out.mask && !out.mask[e])) return;
-    if (out.retry_mode == 2 && !S.rg_retry[2 * e + view]) return;
+    if (out.retry_in && !S.rg_retry[2 * e + view]) return;
     MG_PROF_BEGIN(tid == 0);
-    // capacity overflow: the medium class hands the (env, view) to the large class, else an env error
+    // capacity overflow: a class with a successor hands the (env, view) to it, else an env error
 #define RG_FAIL() do { \
-        if (tid == 0) { if (out.retry_mode == 1) S.rg_retry[2 * e + view] = 1; else S.overflow[e] |= 4 << view; } \
+        if (tid == 0) { if (out.retry_out) S.rg_retry[2 * e + view] = 1; else S.overflow[e] |= 4 << view; } \
         return; } while (0)
     const int nents = S.nents[e];
-    if (nents > SM::RG_MAXE || (out.retry_mode == 1 && out.force_retry)) RG_FAIL();
+    if (nents > SM::RG_MAXE || (out.retry_out && out.force_retry > out.cls_level)) RG_FAIL();
     // ---- 1. geometry list (entity add order x render polys), colour table, view ----
     int my_r0 = 0, my_nr = 0;
     if (tid < nents) {
@@ -476,7 +477,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     }
     RG_SYNC();
     MG_PROF(10);
-    if (out.retry_mode == 2 && tid == 0) S.rg_retry[2 * e + view] = 0;   // every wave has read it (barrier above)
+    if (out.retry_in && tid == 0) S.rg_retry[2 * e + view] = 0;   // every wave has read it (barrier above)
     if (tid == 0) {
         for (int k = 0; k < nents; k++) sm.u.pre.e_g0[k + 1] += sm.u.pre.e_g0[k];
         sm.ngeom = sm.u.pre.e_g0[nents];
@@ -619,6 +620,21 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     RG_SYNC();
     const int nout = sm.bin_off[RG_NBANDS];
     if (nout + sm.ebin_off[RG_NBANDS] > SM::RG_MAXBIN) sm.err = 3;
+#ifdef MG_PROFILE
+    if (tid == 0) {   // scene sizes (tools/gpu_phase.py --sizes): maxima, then counts above candidate caps
+        const unsigned long long nb = (unsigned long long)(nout + sm.ebin_off[RG_NBANDS]);
+        atomicMax(&g_prof[40], (unsigned long long)G); atomicMax(&g_prof[41], (unsigned long long)NV);
+        atomicMax(&g_prof[42], (unsigned long long)sm.ndash); atomicMax(&g_prof[43], (unsigned long long)sm.nsedge);
+        atomicMax(&g_prof[44], nb);
+        if (NV > 768) atomicAdd(&g_prof[45], 1ull);
+        if (NV > 896) atomicAdd(&g_prof[46], 1ull);
+        if (nb > 1536) atomicAdd(&g_prof[47], 1ull);
+        if (G > 48) atomicAdd(&g_prof[48], 1ull);
+        if (sm.ndash > 128) atomicAdd(&g_prof[49], 1ull);
+        if (sm.nsedge > 512) atomicAdd(&g_prof[50], 1ull);
+        atomicAdd(&g_prof[51], 1ull);
+    }
+#endif
     if (tid < RG_NBANDS) { sm.u.pre.bin_cnt[tid] = sm.bin_off[tid]; sm.u.pre.ebin_cnt[tid] = nout + sm.ebin_off[tid]; }
     RG_SYNC();
     if (sm.err) RG_FAIL();

@@ -29,7 +29,7 @@ static int set_err(int code, const std::string &msg) {
 
 struct mg_sim {
     MGState S;
-    int force_render_retry;   // tests: the medium render class hands every (env, view) to the large class
+    int force_render_retry;   // tests: the first k render classes of the chain hand every (env, view) on
     mg_library *dlib;
     void *pool;
     size_t pool_bytes;
@@ -265,7 +265,8 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     s->S.max_tries = 10000; // geom.py:198
     s->S.shw = nullptr;     // HBM-state kernels keep their narrowphase shapes in registers / scratch
     if (const char *mt = getenv("MG_DEBUG_MAX_TRIES")) s->S.max_tries = atoi(mt) > 0 ? atoi(mt) : 10000; // tests only
-    s->force_render_retry = getenv("MG_DEBUG_RENDER_RETRY") != nullptr;                                     // tests only
+    if (const char *rr = getenv("MG_DEBUG_RENDER_RETRY")) s->force_render_retry = atoi(rr);                 // tests only
+    else s->force_render_retry = 0;
     s->S.N = (cfg->num_envs + 63) / 64 * 64;
     Carver sizing = {nullptr, 0};
     layout(s->S, sizing);

@@ -132,9 +132,11 @@ KERNEL_FORMS = [
     ("ClusterShape-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0"}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0"}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "8"}),
-    # render classes of the many-block tasks: the medium class hands every (env, view) to the large one
+    # render classes of the many-block tasks: the first 1 / 2 classes of the chain hand every (env, view) on
     ("ClusterColour-TestAll-LoResStack-v0", 66, 30, {"MG_DEBUG_RENDER_RETRY": "1"}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_DEBUG_RENDER_RETRY": "1"}),
+    ("ClusterColour-TestAll-LoResStack-v0", 66, 30, {"MG_DEBUG_RENDER_RETRY": "2"}),
+    ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_DEBUG_RENDER_RETRY": "2"}),
 ]
 
 
@@ -307,10 +309,11 @@ def test_scores_with_placed_blocks(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,retry", [(c[0], False) for c in CONFIGS] + [("MatchRegions-TestAll-LoRes4E-v0", True)])
+@pytest.mark.parametrize("name,retry", [(c[0], 0) for c in CONFIGS] + [("MatchRegions-TestAll-LoRes4E-v0", 1),
+                                                                     ("MatchRegions-TestAll-LoRes4E-v0", 2)])
 def test_full_resolution_frames(name, retry, monkeypatch):
-    if retry:   # the large render class, through the medium class's hand-over
-        monkeypatch.setenv("MG_DEBUG_RENDER_RETRY", "1")
+    if retry:   # the later render classes, through the earlier classes' hand-over
+        monkeypatch.setenv("MG_DEBUG_RENDER_RETRY", str(retry))
     spec = registry.lookup(name)
     n = 3
     seeds = [7 + i for i in range(n)]

@@ -51,6 +51,10 @@ for view, base in (("allo", 0), ("ego", 16)):
         print(f"   {nm:22s} {v[base + i] / max(tot, 1) * 100:6.1f}%  {v[base + i] / (steps * n):10.0f} ticks/WG")
     for i, nm in enumerate(X):
         print(f"   {nm:22s} {v[base + 5 + i] / (steps * n):10.1f} per WG (sum over bands)")
+if v[51]:
+    print(f"render scene sizes over {v[51]} (env, view) renders: max geoms {v[40]}, vertices {v[41]}, dash lines "
+          f"{v[42]}, solid edges {v[43]}, bin entries {v[44]}; above caps: NV>768 {v[45]}, NV>896 {v[46]}, "
+          f"bins>1536 {v[47]}, geoms>48 {v[48]}, dashes>128 {v[49]}, sedges>512 {v[50]}")
 tot = sum(v[32:40])
 waves = (n + 63) // 64
 print(f"physics: total {tot / 1e6:.1f}M ticks, {waves} waves")
