@@ -363,6 +363,50 @@ MG_DEV bool collide(const ShapeW &A, const ShapeW &B, Collision &info) {
     return sw;
 }
 
+// Exact skip of collide() for shape pairs that are certainly apart.  For convex polygon A, edge k's
+// outward normal n_k (cpPolyShape plane k: the edge ending at vertex k) gives A's largest projection at
+// vertex k; if every point of B (polygon vertices, or the circle's centre) projects more than
+// rA + rB + 1e-9 beyond it, the shapes are farther apart than their radii.  GJK then ends with a
+// distance above rA + rB (its estimate never undercuts the true distance, and 1e-9 is far above its
+// rounding), so collide() returns no contact and touches no arbiter: skipping it changes nothing.
+// A conservative test -- false means "run collide()".  World points as load_shape computes them.
+MG_DEV bool sat_poly_against(const mg_library *L, int pa, double ca, double sa, double pxa, double pya, int pb,
+                             double cb, double sb, double pxb, double pyb, double gap) {
+    const int na = L->poly_count[pa], nb = pb >= 0 ? L->poly_count[pb] : 1;
+    V2 wb[MG_MAX_PVERTS];
+#pragma unroll
+    for (int j = 0; j < MG_MAX_PVERTS; j++) {
+        const double vx = (pb >= 0 && j < nb) ? L->poly_v[pb][j][0] : 0.0;
+        const double vy = (pb >= 0 && j < nb) ? L->poly_v[pb][j][1] : 0.0;
+        wb[j] = v2(cb * vx + (-sb) * vy + pxb, sb * vx + cb * vy + pyb);
+    }
+#pragma unroll
+    for (int k = 0; k < MG_MAX_PVERTS; k++) {
+        if (k >= na) break;
+        const double nx = L->poly_n[pa][k][0], ny = L->poly_n[pa][k][1];
+        const double vx = L->poly_v[pa][k][0], vy = L->poly_v[pa][k][1];
+        const V2 n = v2(ca * nx + (-sa) * ny, sa * nx + ca * ny);
+        const double da = vdot(n, v2(ca * vx + (-sa) * vy + pxa, sa * vx + ca * vy + pya));
+        double mb = INFINITY;
+#pragma unroll
+        for (int j = 0; j < MG_MAX_PVERTS; j++)
+            if (j < nb) mb = cpmin(mb, vdot(n, wb[j]));
+        if (mb - da > gap) return true;
+    }
+    return false;
+}
+MG_DEV bool surely_apart(const MGState &S, const mg_library *L, int e, int i, int j) {
+    const int pi = AT(S.spoly, i), pj = AT(S.spoly, j);
+    if (pi < 0 && pj < 0) return false;   // circle-circle: collide() is cheaper than the test
+    const int bi = AT(S.sbody, i), bj = AT(S.sbody, j);
+    const double gap = AT(S.sr, i) + AT(S.sr, j) + 1e-9;
+    const double ci = AT(S.brc, bi), si = AT(S.brs, bi), xi = AT(S.bpx, bi), yi = AT(S.bpy, bi);
+    const double cj = AT(S.brc, bj), sj = AT(S.brs, bj), xj = AT(S.bpx, bj), yj = AT(S.bpy, bj);
+    if (pi >= 0 && sat_poly_against(L, pi, ci, si, xi, yi, pj, cj, sj, xj, yj, gap)) return true;
+    if (pj >= 0 && sat_poly_against(L, pj, cj, sj, xj, yj, pi, ci, si, xi, yi, gap)) return true;
+    return false;
+}
+
 MG_DEV bool bb_intersects(const ShapeW &a, const ShapeW &b) {
     return (a.bbl <= b.bbr && b.bbl <= a.bbr && a.bbb <= b.bbt && b.bbb <= a.bbt);
 }

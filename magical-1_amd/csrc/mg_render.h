@@ -623,16 +623,16 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
 #ifdef MG_PROFILE
     if (tid == 0) {   // scene sizes (tools/gpu_phase.py --sizes): maxima, then counts above candidate caps
         const unsigned long long nb = (unsigned long long)(nout + sm.ebin_off[RG_NBANDS]);
-        atomicMax(&g_prof[40], (unsigned long long)G); atomicMax(&g_prof[41], (unsigned long long)NV);
-        atomicMax(&g_prof[42], (unsigned long long)sm.ndash); atomicMax(&g_prof[43], (unsigned long long)sm.nsedge);
-        atomicMax(&g_prof[44], nb);
-        if (NV > 768) atomicAdd(&g_prof[45], 1ull);
-        if (NV > 896) atomicAdd(&g_prof[46], 1ull);
-        if (nb > 1536) atomicAdd(&g_prof[47], 1ull);
-        if (G > 48) atomicAdd(&g_prof[48], 1ull);
-        if (sm.ndash > 128) atomicAdd(&g_prof[49], 1ull);
-        if (sm.nsedge > 512) atomicAdd(&g_prof[50], 1ull);
-        atomicAdd(&g_prof[51], 1ull);
+        atomicMax(&g_prof[52], (unsigned long long)G); atomicMax(&g_prof[53], (unsigned long long)NV);
+        atomicMax(&g_prof[54], (unsigned long long)sm.ndash); atomicMax(&g_prof[55], (unsigned long long)sm.nsedge);
+        atomicMax(&g_prof[56], nb);
+        if (NV > 768) atomicAdd(&g_prof[57], 1ull);
+        if (NV > 896) atomicAdd(&g_prof[58], 1ull);
+        if (nb > 1536) atomicAdd(&g_prof[59], 1ull);
+        if (G > 48) atomicAdd(&g_prof[60], 1ull);
+        if (sm.ndash > 128) atomicAdd(&g_prof[61], 1ull);
+        if (sm.nsedge > 512) atomicAdd(&g_prof[62], 1ull);
+        atomicAdd(&g_prof[63], 1ull);
     }
 #endif
     if (tid < RG_NBANDS) { sm.u.pre.bin_cnt[tid] = sm.bin_off[tid]; sm.u.pre.ebin_cnt[tid] = nout + sm.ebin_off[tid]; }

@@ -691,6 +691,7 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
             if (AT(S.sbody, j) == bi) continue;
             int gj = AT(S.sgroup, j);
             if ((gi != 0 && gi == gj) || ((gi | gj) & MG_GROUP_OFF)) continue; // cpShapeFilterReject
+            if (surely_apart(S, L, e, i, j)) continue;                          // no contact (exact skip)
             if (!have_a) { load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A); have_a = true; }
             load_shape(S, L, e, j, (uint64_t)AT(S.shash, j), B);
             Collision info;
@@ -1025,6 +1026,7 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
         int i = 0, j = 0;
         Collision info;
         info.count = 0;
+        int called = 0;
         if (p < total) {
             int lo = 0, hi = ns - 1;
             while (lo < hi) {
@@ -1043,20 +1045,29 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
                     load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A);
                     load_wall(r, W);
                     collide(A, W, info);
+                    called = 1;
                 }
             } else {
                 j = i + 1 + (r - 4);
                 const int gi = AT(S.sgroup, i), gj = AT(S.sgroup, j);
                 if (al <= AT(S.sbbr, j) && AT(S.sbbl, j) <= ar && ab <= AT(S.sbbt, j) && AT(S.sbbb, j) <= at &&
-                    AT(S.sbody, j) != AT(S.sbody, i) && !(gi != 0 && gi == gj) && !((gi | gj) & MG_GROUP_OFF)) {
+                    AT(S.sbody, j) != AT(S.sbody, i) && !(gi != 0 && gi == gj) && !((gi | gj) & MG_GROUP_OFF) &&
+                    !surely_apart(S, L, e, i, j)) {
                     ShapeW A, B;
                     load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A);
                     load_shape(S, L, e, j, (uint64_t)AT(S.shash, j), B);
                     collide(A, B, info);
+                    called = 1;
                 }
             }
         }
         uint64_t m = __ballot(info.count > 0);
+#ifdef MG_PROFILE
+        P.acc[10] += (unsigned long long)__popcll(__ballot(called));
+        P.acc[11] += (unsigned long long)__popcll(m);
+#endif
+        (void)called;
+        MG_PP(P, 8);
         while (m) { // hits in lane order = canonical pair order
             const int src = __ffsll((long long)m) - 1;
             m &= m - 1;
@@ -1084,6 +1095,7 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
                 arbiter_update(S, L, e, key, A, B, AT(S.su, si), ub, c);
             }
         }
+        MG_PP(P, 9);
     }
     __syncthreads();
     MG_PP(P, 2);

@@ -40,7 +40,8 @@ v = list(buf)
 R = ["setup: bin fill", "band clear+prefetch", "band lines", "band fill+resolve", "band output"]
 X = ["max-thread lines work", "max-thread fill work", "long segments", "bin items", "band geoms"]
 P = ["robot_update", "integrate+bb", "broad+narrow", "arb filter", "prestep", "cached impulses", "iterations",
-     "tail(score/reset)"]
+     "tail(score/reset)", "  (broad: pair tests + collide)", "  (broad: arbiter updates)", "  (collide calls)",
+     "  (arbiter updates)"]
 for view, base in (("allo", 0), ("ego", 16)):
     tot = sum(v[base:base + 5]) + sum(v[base + 10:base + 16])
     print(f"render {view}: total {tot / 1e6:.1f}M ticks over {steps} steps x {n} WGs")
@@ -51,13 +52,14 @@ for view, base in (("allo", 0), ("ego", 16)):
         print(f"   {nm:22s} {v[base + i] / max(tot, 1) * 100:6.1f}%  {v[base + i] / (steps * n):10.0f} ticks/WG")
     for i, nm in enumerate(X):
         print(f"   {nm:22s} {v[base + 5 + i] / (steps * n):10.1f} per WG (sum over bands)")
-if v[51]:
-    print(f"render scene sizes over {v[51]} (env, view) renders: max geoms {v[40]}, vertices {v[41]}, dash lines "
-          f"{v[42]}, solid edges {v[43]}, bin entries {v[44]}; above caps: NV>768 {v[45]}, NV>896 {v[46]}, "
-          f"bins>1536 {v[47]}, geoms>48 {v[48]}, dashes>128 {v[49]}, sedges>512 {v[50]}")
-tot = sum(v[32:40])
+if v[63]:
+    print(f"render scene sizes over {v[63]} (env, view) renders: max geoms {v[52]}, vertices {v[53]}, dash lines "
+          f"{v[54]}, solid edges {v[55]}, bin entries {v[56]}; above caps: NV>768 {v[57]}, NV>896 {v[58]}, "
+          f"bins>1536 {v[59]}, geoms>48 {v[60]}, dashes>128 {v[61]}, sedges>512 {v[62]}")
+tot = sum(v[32:42])
 waves = (n + 63) // 64
 print(f"physics: total {tot / 1e6:.1f}M ticks, {waves} waves")
 for i, nm in enumerate(P):
-    print(f"   {nm:22s} {v[32 + i] / max(tot, 1) * 100:6.1f}%  {v[32 + i] / (steps * waves):10.0f} ticks/wave-step")
+    print(f"   {nm:32s} {v[32 + i] / max(tot, 1) * 100:6.1f}%  {v[32 + i] / (steps * waves):10.0f} per wave-step"
+          f"  {v[32 + i] / (steps * n):10.1f} per env-step (cooperative form: one env per wave)")
 vec.close()
