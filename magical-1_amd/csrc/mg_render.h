@@ -29,11 +29,22 @@
 #define RG_MEDIUM2 96, 1280, 160, 2560, 768, MG_MAX_ENTS, uint16_t
 #define RG_SMALL 32, 704, 160, 1536, 256, 6, uint8_t
 #define RG_MAXLONG 16
+#define RG_MAXDE 16                     // dashed edges whose dashes are split over the workgroup
 #define RG_BAND 8
 #define RG_NBANDS (MG_RES / RG_BAND)
 #define RG_THREADS 192                  // = one thread per 4x4 block of a band (2 x 96)
+#ifndef RG_SHORT
 #define RG_SHORT 12                     // segments with <= RG_SHORT * RG_SEGLANES pixels in a band: drawn by
+#endif
+#ifndef RG_SEGLANES
 #define RG_SEGLANES 4                   // their own group of RG_SEGLANES lanes
+#endif
+#ifndef RG_PACK8
+#define RG_PACK8 1                      // fill resolve on 4 byte-packed ordinals per block row (classes with < 127 geoms)
+#endif
+#ifndef RG_DASH_SPLIT
+#define RG_DASH_SPLIT 1                 // dashes of dashed edges split over the workgroup (0: per edge thread)
+#endif
 #define RG_EMPTY 32767
 #define RG_LOROW (MG_LORES * 3)         // bytes of one 96-px RGB row
 #define RG_BANDLO (2 * RG_LOROW)        // bytes of the 2 LoRes rows one band produces
@@ -73,6 +84,9 @@ struct RenderSmem {
     static constexpr int MBITS = 8 * (int)sizeof(MT_), MPW = 4 / (int)sizeof(MT_);   // bits / pixels per word
     static constexpr uint32_t MMASK = (1u << MBITS) - 1u;
     static constexpr bool ORDMAX = MBITS == 32;                                      // layer of ordinals
+    // byte-packed fill resolve: needs ordinals < 256; measured faster on the medium classes (MatchRegions
+    // 3.73 -> 3.68 ms) and slower on the small one (1.245 -> 1.267 ms at 4096 MoveToRegion envs)
+    static constexpr bool PACK8 = RG_PACK8 && MAXG_ > 32 && 2 * MAXG_ + 2 <= 255;
     static_assert(ORDMAX || (MAXE_ <= MBITS && MAXE_ <= MG_MAX_ENTS), "one outline-mask bit per entity");
     union alignas(16) {
         struct {
@@ -85,6 +99,11 @@ struct RenderSmem {
             int32_t bin_cnt[RG_NBANDS], ebin_cnt[RG_NBANDS];
             int16_t g_rpoly[RG_MAXG];
             int16_t e_g0[RG_MAXE + 1];
+            int16_t e_r0[RG_MAXE];                   // first render poly of each entity
+            int32_t ocnt[RG_MAXE];                   // outlined polygons per entity (must be <= 1)
+            double dedge[RG_MAXDE][4];               // dashed outline edges (pixel-space end points) ...
+            int32_t dedge_o[RG_MAXDE];               // ... and their outline-layer value
+            int32_t ndedge;
         } pre;
         struct {
             uint32_t band[RG_BAND][MG_RES / MPW]; // outline layer of the current band (entity bits per pixel)
@@ -102,6 +121,7 @@ struct RenderSmem {
     uint8_t v_geom[RG_MAXVERT];
     uint16_t sedge[RG_MAXSEDGE];              // solid outline edges: start vertex | last << 14 | inside << 15
     int16_t blist[RG_MAXG];                   // geoms overlapping the current band, in draw order
+    uint32_t bxr[RG_MAXG];                    // x range of each band-list slot's geom (ginfo.y)
     int16_t dash[RG_MAXDASH][4];              // clipped dashed-outline lines
     uint16_t dash_o[RG_MAXDASH];              // outline-layer value of each dash line
     int8_t g_ent[RG_MAXG];
@@ -217,32 +237,37 @@ MG_DEV double np_arange_at(double start, double step, int i) {
     return start + i * (next - start);
 }
 
-// render.py:232-255 dashed goal outline, one polygon edge
-template <class SM>
-MG_DEV void push_dashes(SM &sm, double x1, double y1, double x2, double y2, int ord) {
+// render.py:232-255 dashed goal outline of one polygon edge: the two np.arange point sequences
+struct DashSeq { double sx, stx, sy, sty; int n; bool constx, consty; };
+MG_DEV DashSeq dash_seq(double x1, double y1, double x2, double y2) {
     const double dl = 10;
-    double sx, stx, sy, sty;
+    DashSeq d;
     int nx, ny;
-    bool constx = false, consty = false;
+    d.constx = false; d.consty = false;
     if (x1 == x2) {
-        sy = y1; sty = y1 < y2 ? dl : -dl; ny = np_arange_len(y1, y2, sty); nx = ny; constx = true; sx = x1; stx = 0;
+        d.sy = y1; d.sty = y1 < y2 ? dl : -dl; ny = np_arange_len(y1, y2, d.sty); nx = ny; d.constx = true;
+        d.sx = x1; d.stx = 0;
     } else if (y1 == y2) {
-        sx = x1; stx = x1 < x2 ? dl : -dl; nx = np_arange_len(x1, x2, stx); ny = nx; consty = true; sy = y1; sty = 0;
+        d.sx = x1; d.stx = x1 < x2 ? dl : -dl; nx = np_arange_len(x1, x2, d.stx); ny = nx; d.consty = true;
+        d.sy = y1; d.sty = 0;
     } else {
         double a = fabs(x2 - x1), b = fabs(y2 - y1);
         double c = rint(sqrt(a * a + b * b));
         double dx = dl * a / c, dy = dl * b / c;
-        sx = x1; stx = x1 < x2 ? dx : -dx; nx = np_arange_len(x1, x2, stx);
-        sy = y1; sty = y1 < y2 ? dy : -dy; ny = np_arange_len(y1, y2, sty);
+        d.sx = x1; d.stx = x1 < x2 ? dx : -dx; nx = np_arange_len(x1, x2, d.stx);
+        d.sy = y1; d.sty = y1 < y2 ? dy : -dy; ny = np_arange_len(y1, y2, d.sty);
     }
-    int n = nx < ny ? nx : ny;
-    for (int k = 0; 2 * k + 1 < n; k++) {
-        double xa = constx ? sx : np_arange_at(sx, stx, 2 * k + 1);
-        double ya = consty ? sy : np_arange_at(sy, sty, 2 * k + 1);
-        double xb = constx ? sx : np_arange_at(sx, stx, 2 * k);
-        double yb = consty ? sy : np_arange_at(sy, sty, 2 * k);
-        push_wide_line(sm, (int)rint(xa), (int)rint(ya), (int)rint(xb), (int)rint(yb), 4, ord);
-    }
+    d.n = nx < ny ? nx : ny;
+    return d;
+}
+// dash k of the edge: the width-4 line from point 2k + 1 to point 2k (exists when 2k + 1 < n)
+template <class SM>
+MG_DEV void push_dash(SM &sm, const DashSeq &d, int k, int ord) {
+    double xa = d.constx ? d.sx : np_arange_at(d.sx, d.stx, 2 * k + 1);
+    double ya = d.consty ? d.sy : np_arange_at(d.sy, d.sty, 2 * k + 1);
+    double xb = d.constx ? d.sx : np_arange_at(d.sx, d.stx, 2 * k);
+    double yb = d.consty ? d.sy : np_arange_at(d.sy, d.sty, 2 * k);
+    push_wide_line(sm, (int)rint(xa), (int)rint(ya), (int)rint(xb), (int)rint(yb), 4, ord);
 }
 
 template <class SM>
@@ -444,9 +469,11 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         else if (kind == MG_ENT_ROBOT) { my_r0 = L->robot_rpoly0; my_nr = L->robot_nrpoly; }
         else { int t = AT(S.etype, tid); my_r0 = L->block_rpoly0[t]; my_nr = L->block_nrpoly[t]; }
         sm.u.pre.e_g0[tid + 1] = (int16_t)my_nr;
+        sm.u.pre.e_r0[tid] = (int16_t)my_r0;
+        sm.u.pre.ocnt[tid] = 0;
     }
     if (tid == 0) {
-        sm.err = 0; sm.ndash = 0; sm.nsedge = 0; sm.nlong = 0;
+        sm.err = 0; sm.ndash = 0; sm.nsedge = 0; sm.nlong = 0; sm.u.pre.ndedge = 0;
         sm.col[0] = pack_rgb(L->background);
         sm.u.pre.e_g0[0] = 0;
     }
@@ -486,20 +513,25 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     RG_SYNC();
     if (sm.err) RG_FAIL();
     const int G = sm.ngeom;
-    if (tid < nents) {
-        int ecol = AT(S.ecol, tid);
-        for (int k = 0, g = sm.u.pre.e_g0[tid]; k < my_nr; k++, g++) {
-            const mg_rpoly &rp = L->rpoly[my_r0 + k];
-            sm.u.pre.g_rpoly[g] = (int16_t)(my_r0 + k);
-            sm.g_ent[g] = (int8_t)tid;
-            if (rp.outline) {
-                if (sm.oord1[tid + 1]) sm.err = 6;   // two outlined polygons in one entity: the mask needs one
-                sm.oord1[tid + 1] = (uint16_t)(2 * g + 2);
-            }
-            sm.g_nv[g] = (int16_t)rp.npts;
-            sm.col[2 * g + 1] = ref_colour(L, rp.col_ref, ecol);
-            sm.col[2 * g + 2] = rp.outline ? ref_colour(L, rp.ocol_ref, ecol) : 0ull;
+    // one thread per geom: its entity (the last with e_g0 <= g; the reads are independent), render poly,
+    // colours
+    for (int g = tid; g < G; g += RG_THREADS) {
+        int ent = 0;
+#pragma unroll
+        for (int k = 1; k < SM::RG_MAXE; k++) ent += (k < nents && sm.u.pre.e_g0[k] <= g) ? 1 : 0;
+        const int r = sm.u.pre.e_r0[ent] + g - sm.u.pre.e_g0[ent];
+        const mg_rpoly &rp = L->rpoly[r];
+        const int ecol = AT(S.ecol, ent);
+        sm.u.pre.g_rpoly[g] = (int16_t)r;
+        sm.g_ent[g] = (int8_t)ent;
+        if (rp.outline) {
+            // two outlined polygons in one entity: the outline mask has one bit per entity
+            if (atomicAdd(&sm.u.pre.ocnt[ent], 1) != 0) sm.err = 6;
+            sm.oord1[ent + 1] = (uint16_t)(2 * g + 2);
         }
+        sm.g_nv[g] = (int16_t)rp.npts;
+        sm.col[2 * g + 1] = ref_colour(L, rp.col_ref, ecol);
+        sm.col[2 * g + 2] = rp.outline ? ref_colour(L, rp.ocol_ref, ecol) : 0ull;
     }
     RG_SYNC();
     if (tid < 64) wave_exclusive_scan(sm.g_nv, sm.g_voff, G, lane);
@@ -546,7 +578,16 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             double xb, yb;
             rpoly_pt(S, L, e, rp, sm.g_ent[g], j, xb, yb);
             double gxb = __fma_rn(M[1], yb, M[0] * xb) + M[2], gyb = __fma_rn(M[4], yb, M[3] * xb) + M[5];
-            push_dashes(sm, gx, gy, gxb, gyb, SM::ORDMAX ? 2 * g + 2 : 1 << sm.g_ent[g]);
+            const int ord = SM::ORDMAX ? 2 * g + 2 : 1 << sm.g_ent[g];
+            const int q = RG_DASH_SPLIT ? atomicAdd(&sm.u.pre.ndedge, 1) : RG_MAXDE;
+            if (q < RG_MAXDE) {   // dashes drawn below, one thread per dash
+                double *de = sm.u.pre.dedge[q];
+                de[0] = gx; de[1] = gy; de[2] = gxb; de[3] = gyb;
+                sm.u.pre.dedge_o[q] = ord;
+            } else {              // list full: this thread draws the edge's dashes
+                const DashSeq d = dash_seq(gx, gy, gxb, gyb);
+                for (int k = 0; 2 * k + 1 < d.n; k++) push_dash(sm, d, k, ord);
+            }
         }
     }
     RG_SYNC();
@@ -557,6 +598,14 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         int32_t *b = sm.u.pre.gbb[g];
         b[0] = 32767; b[1] = -32768; b[2] = 32767; b[3] = -32768;
         sm.u.pre.gchg[g] = 0;
+    }
+    {   // the dashes of the listed dashed edges: 32 threads per edge, dash k by thread k mod 32
+        const int nde = sm.u.pre.ndedge < RG_MAXDE ? sm.u.pre.ndedge : RG_MAXDE;
+        for (int i = tid; i < 32 * nde; i += RG_THREADS) {
+            const double *de = sm.u.pre.dedge[i >> 5];
+            const DashSeq d = dash_seq(de[0], de[1], de[2], de[3]);
+            for (int k = i & 31; 2 * k + 1 < d.n; k += 32) push_dash(sm, d, k, sm.u.pre.dedge_o[i >> 5]);
+        }
     }
     RG_SYNC();
     for (int v = tid; v < NV; v += RG_THREADS) {
@@ -711,6 +760,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             if (ov) {
                 const int slot = cnt + __popcll(m & ((1ull << lane) - 1ull));
                 sm.blist[slot] = (int16_t)g;
+                sm.bxr[slot] = sm.ginfo[g].y;
                 sm.gslot[g] = (int16_t)slot;
             }
             cnt += __popcll(m);
@@ -820,13 +870,44 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             for (int r = 0; r < 4; r++)
 #pragma unroll
                 for (int c = 0; c < 4; c++) o[r][c] = 0u;
+            // every LDS read of a slot is indexed by the slot alone (no blist -> ginfo chain), so the
+            // reads of successive slots are independent
+            if constexpr (SM::PACK8) {
+                // byte c of orow[r] = ordinal of pixel (x0 + c, row r); a span covers the bytes of columns
+                // [max(l - x0, 0), min(rr - x0, 3)], written with one bitfield insert per row
+                uint32_t orow[4] = {0u, 0u, 0u, 0u};
+#pragma unroll 2
+                for (int slot = 0; slot < ((dskip & 2) ? 0 : nbl); slot++) {
+                    const uint32_t xr = sm.bxr[slot];
+                    const int xmin = (int16_t)(xr & 0xFFFF), xmax = (int16_t)(xr >> 16);
+                    if (xmax < x0 || xmin > x0 + 3) continue;
+                    const uint4 s4 = *(const uint4 *)&sm.bspan[slot][yb];
+                    const uint32_t rep = (2 * (uint32_t)sm.blist[slot] + 1) * 0x01010101u;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const uint32_t spr = r == 0 ? s4.x : r == 1 ? s4.y : r == 2 ? s4.z : s4.w;
+                        const int sa = (int16_t)(spr & 0xFFFF), sb = (int16_t)(spr >> 16);
+                        const int l = sa < sb ? sa : sb, rr = sa < sb ? sb : sa;
+                        // first / one-past-last covered column, clamped to [0, 4]; a row needs an intersection
+                        // on both chains (rr == RG_EMPTY: none)
+                        const int a = min(max(l - x0, 0), 4);
+                        const int b = rr == RG_EMPTY ? 0 : min(max(rr - x0 + 1, 0), 4);
+                        const uint32_t m = (uint32_t)(0xFFFFFFFFull << (8 * a)) & (uint32_t)(0xFFFFFFFFull >> (32 - 8 * b));
+                        orow[r] = (orow[r] & ~m) | (rep & m);
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++) o[r][c] = (orow[r] >> (8 * c)) & 255u;
+            } else
+#pragma unroll 2
             for (int slot = 0; slot < ((dskip & 2) ? 0 : nbl); slot++) {
-                const int g = sm.blist[slot];
-                const uint2 gi = sm.ginfo[g];
-                const int xmin = (int16_t)(gi.y & 0xFFFF), xmax = (int16_t)(gi.y >> 16);
+                const uint32_t xr = sm.bxr[slot];
+                const int xmin = (int16_t)(xr & 0xFFFF), xmax = (int16_t)(xr >> 16);
                 if (xmax < x0 || xmin > x0 + 3) continue;
                 const uint4 s4 = *(const uint4 *)&sm.bspan[slot][yb];
-                const uint32_t ord = 2 * g + 1;
+                const uint32_t ord = 2 * (uint32_t)sm.blist[slot] + 1;
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const uint32_t spr = r == 0 ? s4.x : r == 1 ? s4.y : r == 2 ? s4.z : s4.w;
@@ -839,7 +920,6 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
                 }
             }
             (void)ya;
-            uint64_t sum = 0;
 #pragma unroll
             for (int r = 0; r < ((dskip & 32) ? 0 : 4); r++) {
                 if constexpr (SM::ORDMAX) {
@@ -863,9 +943,14 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
                         }
                     }
                 }
+            }
+            // area sum of the block's 16 colours (a one-lookup path for blocks of one ordinal measured 2% slower:
+            // the 15 compares cost more than the 16 LDS reads they save)
+            uint64_t sum = 0;
+#pragma unroll
+            for (int r = 0; r < 4; r++)
 #pragma unroll
                 for (int c = 0; c < 4; c++) sum += sm.col[o[r][c]];
-            }
             if (mode == 1) {
                 for (int r = 0; r < 4; r++) {
                     uint8_t *dst = out.full + ((((size_t)e * 2 + view) * MG_RES + y0 + yb + r) * MG_RES + x0) * 3;

@@ -9,6 +9,8 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmagical_sim_prof.so" if os.environ.get("MAGICAL_AMD_PROFILE") == "1"
                         else "libmagical_sim.so")
+if os.environ.get("MAGICAL_AMD_EXP_LIB"):   # A/B kernel experiments (tools/gpu_ab.sh): an in-tree build variant
+    LIB_PATH = os.path.join(HERE, "libmagical_sim_%s.so" % os.path.basename(os.environ["MAGICAL_AMD_EXP_LIB"]))
 
 EXPORTS = ["mg_create", "mg_bind_outputs", "mg_reset", "mg_step", "mg_render_full", "mg_get_bodies",
            "mg_set_body_pose", "mg_get_errors", "mg_seed", "mg_random_actions", "mg_num_envs", "mg_enable_timing", "mg_read_timing",
