@@ -87,11 +87,12 @@ def cpu_baseline(name, workers, steps):
 
 
 def load_pmc(kernel, workload, envs):
-    """PMC record of `kernel` (HBM bytes per launch, VALU issue fraction) from the committed passes:
-    profiles/pmc_traffic.json, else profiles/r02_table/<workload>.traffic.json (tools/gpu_table.sh), only
-    when they were collected on this workload and env count."""
-    for path in (os.path.join(ROOT, "profiles", "pmc_traffic.json"),
-                 os.path.join(ROOT, "profiles", "r02_table", f"{workload}.traffic.json")):
+    """PMC record of `kernel` (HBM bytes per launch, VALU issue fraction) from the committed passes, newest
+    first: profiles/r02_final/<workload>.traffic.json (tools/gpu_table.sh at the round's final build), then
+    profiles/r02_table/, then profiles/pmc_traffic.json -- only when collected on this workload and env count."""
+    for path in (os.path.join(ROOT, "profiles", "r02_final", f"{workload}.traffic.json"),
+                 os.path.join(ROOT, "profiles", "r02_table", f"{workload}.traffic.json"),
+                 os.path.join(ROOT, "profiles", "pmc_traffic.json")):
         if not os.path.exists(path):
             continue
         with open(path) as f:

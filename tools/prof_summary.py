@@ -56,16 +56,20 @@ def main():
     if a.traffic_json:
         # FETCH_SIZE / WRITE_SIZE are KiB per dispatch; gfx950 FETCH_SIZE counts half of wide
         # coalesced reads (MI355X_MICROARCH.md, HBM section) -> doubled.
+        # a kernel with several template instances (the render capacity classes, each launched once per
+        # step over the same grid): per-step values are the sums over the instances
         fetch = write = None
         sq = {}
         for db in glob.glob(os.path.join(a.dir, "**", "*.db"), recursive=True):
             for k, cn, n, avg, _ in pmc(db):
-                if k.startswith(a.kernel) and cn == "FETCH_SIZE":
-                    fetch = avg * 1024 * 2
-                if k.startswith(a.kernel) and cn == "WRITE_SIZE":
-                    write = avg * 1024
-                if k.startswith(a.kernel) and (cn.startswith("SQ_") or cn.startswith("GRBM_")):
-                    sq[cn] = avg
+                if not k.startswith(a.kernel):
+                    continue
+                if cn == "FETCH_SIZE":
+                    fetch = (fetch or 0.0) + avg * 1024 * 2
+                if cn == "WRITE_SIZE":
+                    write = (write or 0.0) + avg * 1024
+                if cn.startswith("SQ_") or cn.startswith("GRBM_"):
+                    sq[cn] = sq.get(cn, 0.0) + avg
         data = {}
         if os.path.exists(a.traffic_json):
             data = json.load(open(a.traffic_json))
