@@ -42,6 +42,9 @@
 #ifndef RG_PACK8
 #define RG_PACK8 1                      // fill resolve on 4 byte-packed ordinals per block row (classes with < 127 geoms)
 #endif
+#ifndef RG_SPANW
+#define RG_SPANW 1                      // band spans converted once per slot row to (l, width) before the resolve
+#endif
 #ifndef RG_DASH_SPLIT
 #define RG_DASH_SPLIT 1                 // dashes of dashed edges split over the workgroup (0: per edge thread)
 #endif
@@ -818,6 +821,18 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
                 if (r >= d) { r -= d; q++; }
             }
         }
+        if (RG_SPANW && fwave) {
+            // each row's two chain intersections -> (l, w = r - l); a row missing either intersection is
+            // empty: l = RG_EMPTY, w = 0 (no pixel has x = 32767).  Only this wave writes bspan in the band.
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's span writes are done
+            for (int i = tid - 64; i < nbl * RG_BAND; i += 64) {
+                uint32_t *sp = &sm.bspan[0][0] + i;
+                const uint32_t v = *sp;
+                const int sa = (int16_t)(v & 0xFFFF), sb = (int16_t)(v >> 16);
+                const int l = sa < sb ? sa : sb, rr = sa < sb ? sb : sa;
+                *sp = rr == RG_EMPTY ? (uint32_t)RG_EMPTY : ((uint32_t)(uint16_t)l | ((uint32_t)min(rr - l, 0xFFFF) << 16));
+            }
+        }
         // outline items of this band: solid width-2 edges (clip_and_draw_line_width: base line plus one
         // offset copy, each clipped) and clipped dashed-goal lines
         // (one thread per segment: solid edges contribute two, dash lines one)
@@ -886,12 +901,17 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         const uint32_t spr = r == 0 ? s4.x : r == 1 ? s4.y : r == 2 ? s4.z : s4.w;
-                        const int sa = (int16_t)(spr & 0xFFFF), sb = (int16_t)(spr >> 16);
-                        const int l = sa < sb ? sa : sb, rr = sa < sb ? sb : sa;
-                        // first / one-past-last covered column, clamped to [0, 4]; a row needs an intersection
-                        // on both chains (rr == RG_EMPTY: none)
+                        int l, rr;
+                        if constexpr (RG_SPANW) {   // (l, w); empty rows l = 32767: a = 4, no column
+                            l = (int16_t)(spr & 0xFFFF); rr = l + (int)(spr >> 16);
+                        } else {
+                            const int sa = (int16_t)(spr & 0xFFFF), sb = (int16_t)(spr >> 16);
+                            l = sa < sb ? sa : sb; rr = sa < sb ? sb : sa;
+                            if (rr == RG_EMPTY) rr = -1;   // a row needs an intersection on both chains
+                        }
+                        // first / one-past-last covered column, clamped to [0, 4]
                         const int a = min(max(l - x0, 0), 4);
-                        const int b = rr == RG_EMPTY ? 0 : min(max(rr - x0 + 1, 0), 4);
+                        const int b = min(max(rr - x0 + 1, 0), 4);
                         const uint32_t m = (uint32_t)(0xFFFFFFFFull << (8 * a)) & (uint32_t)(0xFFFFFFFFull >> (32 - 8 * b));
                         orow[r] = (orow[r] & ~m) | (rep & m);
                     }
@@ -911,12 +931,21 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const uint32_t spr = r == 0 ? s4.x : r == 1 ? s4.y : r == 2 ? s4.z : s4.w;
-                    const int sa = (int16_t)(spr & 0xFFFF), sb = (int16_t)(spr >> 16);
-                    const int l = sa < sb ? sa : sb, rr = sa < sb ? sb : sa;
-                    if (rr == RG_EMPTY) continue;   // a row needs an intersection on both chains
+                    if constexpr (RG_SPANW) {
+                        // pixel x covered iff 0 <= x - l <= w (unsigned compare; empty rows: l = 32767, w = 0)
+                        const int l = (int16_t)(spr & 0xFFFF);
+                        const uint32_t w = spr >> 16;
 #pragma unroll
-                    for (int c = 0; c < 4; c++)
-                        if (x0 + c >= l && x0 + c <= rr) o[r][c] = ord;
+                        for (int c = 0; c < 4; c++)
+                            o[r][c] = (uint32_t)(x0 + c - l) <= w ? ord : o[r][c];
+                    } else {
+                        const int sa = (int16_t)(spr & 0xFFFF), sb = (int16_t)(spr >> 16);
+                        const int l = sa < sb ? sa : sb, rr = sa < sb ? sb : sa;
+                        if (rr == RG_EMPTY) continue;   // a row needs an intersection on both chains
+#pragma unroll
+                        for (int c = 0; c < 4; c++)
+                            if (x0 + c >= l && x0 + c <= rr) o[r][c] = ord;
+                    }
                 }
             }
             (void)ya;
