@@ -45,10 +45,14 @@
 #ifndef RG_SPANW
 #define RG_SPANW 1                      // band spans converted once per slot row to (l, width) before the resolve
 #endif
+#ifndef RG_OFS
+#define RG_OFS 1                        // resolve ordinals carried as byte offsets into the colour table (x8)
+#endif
 #ifndef RG_DASH_SPLIT
 #define RG_DASH_SPLIT 1                 // dashes of dashed edges split over the workgroup (0: per edge thread)
 #endif
 #define RG_EMPTY 32767
+#define RG_OSH (RG_OFS ? 3 : 0)         // resolve/outline-layer ordinal values are ordinal << RG_OSH
 #define RG_LOROW (MG_LORES * 3)         // bytes of one 96-px RGB row
 #define RG_BANDLO (2 * RG_LOROW)        // bytes of the 2 LoRes rows one band produces
 #define RG_BANDLO16 (RG_BANDLO / 16)    // ... in 16-byte chunks (36)
@@ -359,7 +363,7 @@ MG_DEV void edge_ends(const SM &sm, int k, int &x1, int &y1, int &x2, int &y2, u
     x1 = sm.vx[v] + (fd & 3) - 1; y1 = sm.vy[v] + ((fd >> 2) & 3) - 1;
     if (se & 0x4000u) { const int nx = sm.g_voff[g]; x2 = sm.vx[nx]; y2 = sm.vy[nx]; } // closing edge
     else { x2 = sm.vx[v + 1]; y2 = sm.vy[v + 1]; }
-    ord = SM::ORDMAX ? 2 * g + 2 : 1u << sm.g_ent[g];   // the outline layer's value
+    ord = SM::ORDMAX ? (2u * g + 2) << RG_OSH : 1u << sm.g_ent[g];   // the outline layer's value
     inside = (se & 0x8000u) != 0;
 }
 
@@ -530,7 +534,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         if (rp.outline) {
             // two outlined polygons in one entity: the outline mask has one bit per entity
             if (atomicAdd(&sm.u.pre.ocnt[ent], 1) != 0) sm.err = 6;
-            sm.oord1[ent + 1] = (uint16_t)(2 * g + 2);
+            sm.oord1[ent + 1] = (uint16_t)((2 * g + 2) << RG_OSH);
         }
         sm.g_nv[g] = (int16_t)rp.npts;
         sm.col[2 * g + 1] = ref_colour(L, rp.col_ref, ecol);
@@ -581,7 +585,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
             double xb, yb;
             rpoly_pt(S, L, e, rp, sm.g_ent[g], j, xb, yb);
             double gxb = __fma_rn(M[1], yb, M[0] * xb) + M[2], gyb = __fma_rn(M[4], yb, M[3] * xb) + M[5];
-            const int ord = SM::ORDMAX ? 2 * g + 2 : 1 << sm.g_ent[g];
+            const int ord = SM::ORDMAX ? (2 * g + 2) << RG_OSH : 1 << sm.g_ent[g];
             const int q = RG_DASH_SPLIT ? atomicAdd(&sm.u.pre.ndedge, 1) : RG_MAXDE;
             if (q < RG_MAXDE) {   // dashes drawn below, one thread per dash
                 double *de = sm.u.pre.dedge[q];
@@ -919,7 +923,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
 #pragma unroll
                 for (int r = 0; r < 4; r++)
 #pragma unroll
-                    for (int c = 0; c < 4; c++) o[r][c] = (orow[r] >> (8 * c)) & 255u;
+                    for (int c = 0; c < 4; c++) o[r][c] = ((orow[r] >> (8 * c)) & 255u) << RG_OSH;
             } else
 #pragma unroll 2
             for (int slot = 0; slot < ((dskip & 2) ? 0 : nbl); slot++) {
@@ -927,7 +931,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
                 const int xmin = (int16_t)(xr & 0xFFFF), xmax = (int16_t)(xr >> 16);
                 if (xmax < x0 || xmin > x0 + 3) continue;
                 const uint4 s4 = *(const uint4 *)&sm.bspan[slot][yb];
-                const uint32_t ord = 2 * (uint32_t)sm.blist[slot] + 1;
+                const uint32_t ord = (2 * (uint32_t)sm.blist[slot] + 1) << RG_OSH;
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const uint32_t spr = r == 0 ? s4.x : r == 1 ? s4.y : r == 2 ? s4.z : s4.w;
@@ -979,20 +983,21 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
 #pragma unroll
             for (int r = 0; r < 4; r++)
 #pragma unroll
-                for (int c = 0; c < 4; c++) sum += sm.col[o[r][c]];
+                for (int c = 0; c < 4; c++) sum += *(const uint64_t *)((const char *)sm.col + (o[r][c] << (3 - RG_OSH)));
             if (mode == 1) {
                 for (int r = 0; r < 4; r++) {
                     uint8_t *dst = out.full + ((((size_t)e * 2 + view) * MG_RES + y0 + yb + r) * MG_RES + x0) * 3;
                     for (int c = 0; c < 4; c++) {
-                        const uint64_t cc = sm.col[o[r][c]];
+                        const uint64_t cc = *(const uint64_t *)((const char *)sm.col + (o[r][c] << (3 - RG_OSH)));
                         dst[3 * c] = (uint8_t)cc; dst[3 * c + 1] = (uint8_t)(cc >> 16); dst[3 * c + 2] = (uint8_t)(cc >> 32);
                     }
                 }
             } else {
                 for (int ch = 0; ch < ((dskip & 256) ? 0 : 3); ch++) {
                     const int ss = (int)((sum >> (16 * ch)) & 0xFFFF);
-                    const int q = ss >> 4, rm = ss & 15;
-                    lo8[lpix * 3 + ch] = (uint8_t)(q + (rm > 8 || (rm == 8 && (q & 1))));
+                    // round half to even of ss / 16: + 7, + 1 more when ss / 16 is odd
+                    if (RG_OFS) lo8[lpix * 3 + ch] = (uint8_t)((ss + 7 + ((ss >> 4) & 1)) >> 4);
+                    else { const int q = ss >> 4, rm = ss & 15; lo8[lpix * 3 + ch] = (uint8_t)(q + (rm > 8 || (rm == 8 && (q & 1)))); }
                 }
             }
         }
