@@ -48,6 +48,9 @@
 #ifndef RG_OFS
 #define RG_OFS 1                        // resolve ordinals carried as byte offsets into the colour table (x8)
 #endif
+#ifndef RG_XF_LATE
+#define RG_XF_LATE 1                    // entity transforms / view matrix overlap the geometry table (one barrier fewer)
+#endif
 #ifndef RG_DASH_SPLIT
 #define RG_DASH_SPLIT 1                 // dashes of dashed edges split over the workgroup (0: per edge thread)
 #endif
@@ -486,6 +489,7 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     }
     if (tid < RG_NBANDS) { sm.u.pre.bin_cnt[tid] = 0; sm.u.pre.ebin_cnt[tid] = 0; }
     if (tid < 17) sm.oord1[tid] = 0;
+#if !RG_XF_LATE
     if (view == 0 && tid == 32) { // Viewer.render: stack.push(self.transform) -> eye(3) @ view
         const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
         mg_mat3_mul(I3, L->allo_view, sm.u.pre.view);
@@ -509,9 +513,44 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
         if (x == MG_XF_MAIN || AT(S.ekind, ent) == MG_ENT_ROBOT)   // one robot per scene
             entity_xform(S, e, ent, x, sm.u.pre.e_xf[xf_slot<SM>(ent, x)]);
     }
+#endif
     RG_SYNC();
     MG_PROF(10);
     if (out.retry_in && tid == 0) S.rg_retry[2 * e + view] = 0;   // every wave has read it (barrier above)
+#if RG_XF_LATE
+    // every thread forms the entities' first-geom offsets itself from the per-entity counts (independent
+    // LDS reads, no barrier); the entity transforms and the view matrix (long serial f64 chains, correctly
+    // rounded sincos for the pupils) run here, beside the geometry table's global loads
+    int goff[SM::RG_MAXE + 1];
+    goff[0] = 0;
+#pragma unroll
+    for (int k = 0; k < SM::RG_MAXE; k++) goff[k + 1] = goff[k] + (k < nents ? (int)sm.u.pre.e_g0[k + 1] : 0);
+    const int G = goff[SM::RG_MAXE];
+    if (G > SM::RG_MAXG) RG_FAIL();
+    if (view == 0 && tid == RG_THREADS - 1) { // Viewer.render: stack.push(self.transform) -> eye(3) @ view
+        const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        mg_mat3_mul(I3, L->allo_view, sm.u.pre.view);
+    }
+    if (view == 1 && tid == RG_THREADS - 1) {
+        // Viewer.set_cam_follow / ego_cam_matrix: P @ (scale @ (tr1 @ (rot @ tr2)))
+        int rb = S.robot_body0[e];
+        double rot[9], tr2[9], m1[9], m2[9], m3[9], sn, cs;
+        body_sincos(S, e, rb, sn, cs); // sincos(-a) = (-sin a, cos a): a correctly rounded sin is odd
+        mg_transform_tr_sc(0.0, 0.0, -sn, cs, rot);
+        mg_transform_tr(-AT(S.bpx, rb), -AT(S.bpy, rb), 0.0, tr2);
+        mg_mat3_mul(rot, tr2, m1);
+        mg_mat3_mul(L->ego_tr1_m, m1, m2);
+        mg_mat3_mul(L->ego_scale_m, m2, m3);
+        mg_mat3_mul(L->pygame_m, m3, m1);
+        const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        mg_mat3_mul(I3, m1, sm.u.pre.view);
+    }
+    if (tid >= 64 && tid - 64 < 5 * nents) {
+        const int ent = (tid - 64) / 5, x = (tid - 64) % 5;
+        if (x == MG_XF_MAIN || AT(S.ekind, ent) == MG_ENT_ROBOT)   // one robot per scene
+            entity_xform(S, e, ent, x, sm.u.pre.e_xf[xf_slot<SM>(ent, x)]);
+    }
+#else
     if (tid == 0) {
         for (int k = 0; k < nents; k++) sm.u.pre.e_g0[k + 1] += sm.u.pre.e_g0[k];
         sm.ngeom = sm.u.pre.e_g0[nents];
@@ -520,13 +559,21 @@ __global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_
     RG_SYNC();
     if (sm.err) RG_FAIL();
     const int G = sm.ngeom;
-    // one thread per geom: its entity (the last with e_g0 <= g; the reads are independent), render poly,
-    // colours
+#endif
+    // one thread per geom: its entity (the last with a first geom <= g; the reads are independent), render
+    // poly, colours
     for (int g = tid; g < G; g += RG_THREADS) {
-        int ent = 0;
+        int ent = 0, g0 = 0;
 #pragma unroll
-        for (int k = 1; k < SM::RG_MAXE; k++) ent += (k < nents && sm.u.pre.e_g0[k] <= g) ? 1 : 0;
-        const int r = sm.u.pre.e_r0[ent] + g - sm.u.pre.e_g0[ent];
+        for (int k = 1; k < SM::RG_MAXE; k++) {
+#if RG_XF_LATE
+            const int gk = goff[k];
+#else
+            const int gk = sm.u.pre.e_g0[k];
+#endif
+            if (k < nents && gk <= g) { ent = k; g0 = gk; }
+        }
+        const int r = sm.u.pre.e_r0[ent] + g - g0;
         const mg_rpoly &rp = L->rpoly[r];
         const int ecol = AT(S.ecol, ent);
         sm.u.pre.g_rpoly[g] = (int16_t)r;
