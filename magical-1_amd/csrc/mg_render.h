@@ -456,8 +456,14 @@ template <class SM>
 MG_DEV int xf_slot(int ent, int x) { return x == MG_XF_MAIN ? ent : SM::RG_MAXE + x - 1; }
 
 // One (env, view) per workgroup.  mode 0: LoRes outputs; mode 1: full-resolution frames.
+#ifndef RG_SMALL_WPE
+#define RG_SMALL_WPE 7                  // waves per SIMD the small class is compiled for: 72 VGPRs, 9 workgroups/CU
+                                        // (measured: 7 -> 2.5% faster than the default 6; 8 = 64 VGPRs slower)
+#endif
 template <class SM, int MODE>
-__global__ void __launch_bounds__(RG_THREADS) render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
+__global__ void __launch_bounds__(RG_THREADS)
+__attribute__((amdgpu_waves_per_eu((SM::RG_MAXG <= 32 && RG_SMALL_WPE) ? RG_SMALL_WPE : 1)))
+render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     __shared__ SM sm;
     constexpr int mode = MODE;
     const int e = blockIdx.x, view = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
