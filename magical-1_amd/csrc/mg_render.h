@@ -39,9 +39,6 @@
 #ifndef RG_SEGLANES
 #define RG_SEGLANES 4                   // their own group of RG_SEGLANES lanes
 #endif
-#ifndef RG_PACK8
-#define RG_PACK8 1                      // fill resolve on 4 byte-packed ordinals per block row (classes with < 127 geoms)
-#endif
 #ifndef RG_SPANW
 #define RG_SPANW 1                      // band spans converted once per slot row to (l, width) before the resolve
 #endif
@@ -94,9 +91,6 @@ struct RenderSmem {
     static constexpr int MBITS = 8 * (int)sizeof(MT_), MPW = 4 / (int)sizeof(MT_);   // bits / pixels per word
     static constexpr uint32_t MMASK = (1u << MBITS) - 1u;
     static constexpr bool ORDMAX = MBITS == 32;                                      // layer of ordinals
-    // byte-packed fill resolve: needs ordinals < 256; measured faster on the medium classes (MatchRegions
-    // 3.73 -> 3.68 ms) and slower on the small one (1.245 -> 1.267 ms at 4096 MoveToRegion envs)
-    static constexpr bool PACK8 = RG_PACK8 && MAXG_ > 32 && 2 * MAXG_ + 2 <= 255;
     static_assert(ORDMAX || (MAXE_ <= MBITS && MAXE_ <= MG_MAX_ENTS), "one outline-mask bit per entity");
     union alignas(16) {
         struct {
@@ -944,40 +938,6 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                 for (int c = 0; c < 4; c++) o[r][c] = 0u;
             // every LDS read of a slot is indexed by the slot alone (no blist -> ginfo chain), so the
             // reads of successive slots are independent
-            if constexpr (SM::PACK8) {
-                // byte c of orow[r] = ordinal of pixel (x0 + c, row r); a span covers the bytes of columns
-                // [max(l - x0, 0), min(rr - x0, 3)], written with one bitfield insert per row
-                uint32_t orow[4] = {0u, 0u, 0u, 0u};
-#pragma unroll 2
-                for (int slot = 0; slot < ((dskip & 2) ? 0 : nbl); slot++) {
-                    const uint32_t xr = sm.bxr[slot];
-                    const int xmin = (int16_t)(xr & 0xFFFF), xmax = (int16_t)(xr >> 16);
-                    if (xmax < x0 || xmin > x0 + 3) continue;
-                    const uint4 s4 = *(const uint4 *)&sm.bspan[slot][yb];
-                    const uint32_t rep = (2 * (uint32_t)sm.blist[slot] + 1) * 0x01010101u;
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const uint32_t spr = r == 0 ? s4.x : r == 1 ? s4.y : r == 2 ? s4.z : s4.w;
-                        int l, rr;
-                        if constexpr (RG_SPANW) {   // (l, w); empty rows l = 32767: a = 4, no column
-                            l = (int16_t)(spr & 0xFFFF); rr = l + (int)(spr >> 16);
-                        } else {
-                            const int sa = (int16_t)(spr & 0xFFFF), sb = (int16_t)(spr >> 16);
-                            l = sa < sb ? sa : sb; rr = sa < sb ? sb : sa;
-                            if (rr == RG_EMPTY) rr = -1;   // a row needs an intersection on both chains
-                        }
-                        // first / one-past-last covered column, clamped to [0, 4]
-                        const int a = min(max(l - x0, 0), 4);
-                        const int b = min(max(rr - x0 + 1, 0), 4);
-                        const uint32_t m = (uint32_t)(0xFFFFFFFFull << (8 * a)) & (uint32_t)(0xFFFFFFFFull >> (32 - 8 * b));
-                        orow[r] = (orow[r] & ~m) | (rep & m);
-                    }
-                }
-#pragma unroll
-                for (int r = 0; r < 4; r++)
-#pragma unroll
-                    for (int c = 0; c < 4; c++) o[r][c] = ((orow[r] >> (8 * c)) & 255u) << RG_OSH;
-            } else
 #pragma unroll 2
             for (int slot = 0; slot < ((dskip & 2) ? 0 : nbl); slot++) {
                 const uint32_t xr = sm.bxr[slot];
