@@ -25,7 +25,9 @@
 // per entity).  The large class fits every task; the small one fits robot + arena + goal + one block
 // (MoveToRegion / MoveToCorner) and leaves room for 9 workgroups/CU.
 #define RG_LARGE 160, 1600, 256, 3072, 1600, MG_MAX_ENTS, uint32_t
+#ifndef RG_MEDIUM1
 #define RG_MEDIUM1 48, 896, 160, 1536, 512, MG_MAX_ENTS, uint16_t
+#endif
 #define RG_MEDIUM2 96, 1280, 160, 2560, 768, MG_MAX_ENTS, uint16_t
 #define RG_SMALL 32, 704, 160, 1536, 256, 6, uint8_t
 #define RG_MAXLONG 16
