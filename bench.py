@@ -12,15 +12,23 @@ training stream does.  Actions come from device Philox (key 42, counter =
 (step, env)).  Multi-GPU: one process per GPU, envs sharded contiguously
 (global env id = rank * envs + i, seed 1000 + id), no data-path collective
 (instances are independent) -> weak scaling; the timed region is bracketed by
-barrier + synchronize and the max over ranks is reported.  --gather adds the north
-star's exchange: each step's results (obs, reward, done, eval_score) of every rank
-all-gathered to every rank as one packed buffer over RCCL, on its own stream,
-overlapping the next step (magical_amd.dist).
+barrier + synchronize and the max over ranks is reported.  `--gpus N` with N > 1
+(and no WORLD_SIZE in the environment) launches the N ranks itself through
+torch.distributed.run, before anything touches a GPU.  For N > 1 the north star's
+exchange is on by default (--no-gather turns it off): each step's results of every
+rank reach every rank through one packed RCCL all-gather on a side stream,
+overlapping the next step; by default only the current LoRes frames plus
+reward/done/eval_score are gathered and every receiver rebuilds the frame stacks
+(mg_restack), --gather-mode stacked gathers the whole observations
+(magical_amd.dist).  --dry-run checks the launcher and the process group (gloo, no
+GPU): rank 0 prints {"ranks_seen": N}.
 """
 import argparse
 import json
 import multiprocessing as mp
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,9 +38,48 @@ sys.path[:0] = [os.path.join(ROOT, "magical-1_amd"), os.path.join(ROOT, "oracle"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
 
 
+FR = 96 * 96 * 3            # one LoRes RGB frame
+STATE_BYTES = 2048          # per-env state read + written once per env-step (~2 KB)
+
+
 def obs_bytes(preproc):
     return {"LoRes4E": 165888, "LoRes4A": 165888, "LoRes3EA": 165888, "LoResCHW4E": 165888, "LoResCHW4A": 165888,
             "LoResStack": 221184}.get(preproc, 2 * 384 * 384 * 3)
+
+
+def render_bytes(preproc, frames_only=False):
+    """Bytes the render kernel must move per env-step: the observation outputs, plus the frame ring of
+    each stacked view (3 earlier frames read, the current one written; the 4 slots are filled at reset).
+    frames_only (compact multi-GPU gather): the two current frames only -- the stacks are rebuilt by
+    mg_restack on the receivers."""
+    if frames_only:
+        return 2 * FR
+    stacked_views = {"LoResStack": 2, "LoRes4E": 1, "LoRes4A": 1, "LoResCHW4E": 1, "LoResCHW4A": 1}.get(preproc, 0)
+    ring = stacked_views * 4 * FR
+    if preproc == "LoRes3EA":   # ego ring (1 write) + compose pass (allo + 3 ring frames read, 4 frames written)
+        ring = FR + 4 * FR + 4 * FR
+    return obs_bytes(preproc) + ring
+
+
+def restack_bytes(preproc):
+    """mg_restack per received env-step: current frame read, 3 ring frames read, 1 ring frame written and
+    the 4-frame stack written, per stacked view (LoRes3EA: + the allo frame read)."""
+    views = 2 if preproc == "LoResStack" else 1
+    return views * (FR + 3 * FR + FR + 4 * FR) + (FR if preproc == "LoRes3EA" else 0)
+
+
+def cpu_share():
+    """CPUs this job may use: the affinity mask, capped by a cgroup v2 quota when one is set."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
 
 
 def _cpu_worker(args):
@@ -62,10 +109,10 @@ def _pool_run(name, workers, steps):
     return sum(r[0] for r in res) / wall, sum(r[0] / r[1] for r in res) / workers, wall
 
 
-def cpu_baseline(name, workers, steps):
+def cpu_baseline(name, workers, steps, affinity, quota):
     """The C oracle restatement (1 env per process, resets included) on 1 core and on `workers`
-    cores of this host.  On the GPU box `workers` is the job's CPU share (16 of the host's CPUs);
-    the whole-host figure is the per-core rate times the host's CPU count, labelled as scaled."""
+    processes = every CPU this job may use (affinity mask, capped by the cgroup quota), measured.
+    The whole-host figure is the per-core rate times the host's CPU count, labelled as scaled."""
     one, _, wall1 = _pool_run(name, 1, 2 * steps)
     many, per_core, wall = _pool_run(name, workers, steps)
     cpu_model = "unknown"
@@ -79,6 +126,7 @@ def cpu_baseline(name, workers, steps):
             "cpu_model": cpu_model, "host_cpus": host,
             "sample": f"C oracle restatement of {name}, 1 env per process incl. resets: 1 process x {2 * steps} "
                       f"steps (wall {wall1:.1f}s), then {workers} processes x {steps} steps (wall {wall:.1f}s)",
+            "affinity_cpus": affinity, "cgroup_quota_cpus": quota,
             "one_core_env_steps_s": round(one, 1),
             "per_core_env_steps_s": round(per_core, 1),
             "host_scaled_env_steps_s": round(per_core * host, 1),
@@ -90,7 +138,8 @@ def load_pmc(kernel, workload, envs):
     """PMC record of `kernel` (HBM bytes per launch, VALU issue fraction) from the committed passes, newest
     first: profiles/r02_final/<workload>.traffic.json (tools/gpu_table.sh at the round's final build), then
     profiles/r02_table/, then profiles/pmc_traffic.json -- only when collected on this workload and env count."""
-    for path in (os.path.join(ROOT, "profiles", "r02_final", f"{workload}.traffic.json"),
+    for path in (os.path.join(ROOT, "profiles", "r03_final", f"{workload}.traffic.json"),
+                 os.path.join(ROOT, "profiles", "r02_final", f"{workload}.traffic.json"),
                  os.path.join(ROOT, "profiles", "r02_table", f"{workload}.traffic.json"),
                  os.path.join(ROOT, "profiles", "pmc_traffic.json")):
         if not os.path.exists(path):
@@ -102,6 +151,33 @@ def load_pmc(kernel, workload, envs):
     return None
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """One process per GPU: re-run this script under torch.distributed.run with n ranks (rendezvous on
+    127.0.0.1) and return its exit code.  Called before anything in this process touches a GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1")))
+
+
+def kernel_record(name, ms, bytes_per_env, n, pmc):
+    """One kernel's roofline figures: algorithmic bytes per launch over its HIP-event average duration."""
+    if ms is None or ms <= 0:
+        return None
+    ach = bytes_per_env * n / (ms * 1e-3) / 1e9
+    return {"ms": round(ms, 4), "bytes_per_env_step": bytes_per_env, "achieved_gbs": round(ach, 2),
+            "hbm_frac": round(ach / HBM_PEAK_GBS, 5),
+            "traffic_bytes_per_launch": pmc and pmc.get("bytes_per_launch"),
+            "valu_issue_frac": pmc and pmc.get("valu_issue_frac"), "wait_any_frac": pmc and pmc.get("wait_any_frac")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,24 +185,47 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs", type=int, default=4096, help="env instances per GPU")
     ap.add_argument("--env", default="MoveToRegion-Demo-LoRes4E-v0")
-    ap.add_argument("--cpu-workers", type=int, default=16)
-    ap.add_argument("--cpu-steps", type=int, default=1500)  # ~16 x 1 s of CPU work (about 15-25 s)
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0: every CPU this job may use")
+    ap.add_argument("--cpu-steps", type=int, default=1500)  # ~1-2 s of CPU work per process
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--gather", action="store_true",
-                    help="N > 1: all-gather every step's packed results (obs, reward, done, score) to every rank "
-                         "(the north star's exchange; magical_amd.dist.ShardedVecEnv), pipelined with the next step")
+    ap.add_argument("--gather", dest="gather", action="store_true", default=None,
+                    help="all-gather every step's results to every rank (default for N > 1)")
+    ap.add_argument("--no-gather", dest="gather", action="store_false")
+    ap.add_argument("--gather-mode", default="frames", choices=("frames", "stacked"),
+                    help="frames: current frames + scalars, stacks rebuilt on each receiver; stacked: whole obs")
     ap.add_argument("--no-phase-spread", action="store_true",
                     help="start every env at episode step 0 (resets then happen on the same step for all envs)")
+    ap.add_argument("--dry-run", action="store_true", help="launcher / process-group check only (gloo, no GPU)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:   # an outside launcher decides the world size; --gpus is informational then
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; using {world} ranks", file=sys.stderr)
+
+    if args.dry_run:
+        import torch
+        import torch.distributed as dist
+        if world > 1:
+            dist.init_process_group("gloo")
+        t = torch.ones(1)
+        if world > 1:
+            dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": args.gpus, "ranks_seen": int(t.item()),
+                              "gather": args.gather if args.gather is not None else world > 1}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
-        cpu = cpu_baseline(args.env, workers, args.cpu_steps)
+        share, affinity, quota = cpu_share()
+        workers = args.cpu_workers or share
+        cpu = cpu_baseline(args.env, workers, args.cpu_steps, affinity, quota)
 
     import torch
     import torch.distributed as dist
@@ -140,10 +239,11 @@ def main():
         dist.init_process_group("nccl", device_id=device)
     n = args.envs
     seeds = [1000 + rank * n + i for i in range(n)]
-    gather = args.gather and world > 1
+    gather = (world > 1) if args.gather is None else (args.gather and world > 1)
     if gather:
         from magical_amd import dist as mdist
-        shard = mdist.ShardedVecEnv(args.env, n, rank=rank, device=str(device), gather=True)
+        shard = mdist.ShardedVecEnv(args.env, n, rank=rank, device=str(device), gather=True,
+                                    gather_mode=args.gather_mode)
         vec = shard.vec
         step = shard.step_async
     else:
@@ -163,9 +263,7 @@ def main():
         vec.random_actions(s, out=actions)
         step(actions)
     if gather:
-        for h in shard.pending:
-            if h is not None:
-                h.wait()
+        shard.wait_all()
     torch.cuda.synchronize(device)
     native.check(lib.mg_enable_timing(vec.handle, args.steps))
     if world > 1:
@@ -175,10 +273,8 @@ def main():
     for s in range(args.steps):
         vec.random_actions(args.warmup + s, out=actions)
         step(actions)
-    if gather:   # the timed region ends after the last step's gather
-        for h in shard.pending:
-            if h is not None:
-                h.wait()
+    if gather:   # the timed region ends after the last step's exchange (all-gather + restack)
+        shard.wait_all()
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -189,25 +285,31 @@ def main():
     t_step_ms, t_render_ms, n_timed = tm[0] / args.steps, tm[1] / args.steps, int(tm[2])
     t_reset_ms = tm[3] / args.steps
     errors = int((vec.errors() != 0).sum().item())
+    ranks_seen = world
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        e = torch.tensor([errors], dtype=torch.int64, device=device)
+        e = torch.tensor([errors, 1], dtype=torch.int64, device=device)
         dist.all_reduce(e)
-        errors = int(e.item())
+        errors, ranks_seen = int(e[0].item()), int(e[1].item())
     value = world * n * args.steps / elapsed
     if rank == 0:
-        per_env = obs_bytes(spec.preproc) + 2048  # obs bytes + ~2 KB state per env-step
+        frames_only = gather and args.gather_mode == "frames"
+        kernels = {
+            "render_kernel": kernel_record("render_kernel", t_render_ms, render_bytes(spec.preproc, frames_only), n,
+                                           load_pmc("render_kernel", args.env, n)),
+            "step_kernel": kernel_record("step_kernel", t_step_ms, STATE_BYTES, n, load_pmc("step_kernel", args.env, n)),
+            "reset_kernel": {"ms": round(t_reset_ms, 4)},
+        }
         dom = "render_kernel" if t_render_ms >= t_step_ms else "step_kernel"
-        dom_ms = max(t_render_ms, t_step_ms)
-        achieved = per_env * n / (dom_ms * 1e-3) / 1e9
-        pmc = load_pmc(dom, args.env, n)
+        dk = kernels[dom]
         out = {
             "metric": "env-steps/sec (whole node) at N instances/GPU, 1/2/4/8 MI355X",
             "value": round(value, 1),
             "unit": "env-steps/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -219,22 +321,25 @@ def main():
             "config": {"workload": args.env, "envs_per_gpu": n, "episode_steps": spec.max_episode_steps,
                        "physics_substeps": 10, "solver_iterations": 10, "render": "2 x 384^2 -> 96^2",
                        "phase_spread": phase_spread,
-                       "parallelism": (f"dp{world} (envs sharded; one packed all-gather of every step's results, "
+                       "parallelism": (f"dp{world} (envs sharded; one packed all-gather per step ({args.gather_mode}), "
                                        f"pipelined with the next step)" if gather else
                                        f"dp{world} (envs sharded, no data-path collective)")},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": pmc and pmc["bytes_per_launch"], "bytes_per_env_step": per_env,
-                         "units_per_launch": n, "kernel_avg_ms": round(dom_ms, 4),
-                         # the binding resource is VALU issue, not HBM: SQ_INSTS_VALU x 2 cycles over
-                         # 1024 SIMDs x GRBM_GUI_ACTIVE / 8 of the committed SQ pass (profiles/)
-                         "valu_issue_frac": pmc and pmc.get("valu_issue_frac"),
-                         "wait_any_frac": pmc and pmc.get("wait_any_frac")},
+            # dominant kernel against HBM with ITS OWN algorithmic bytes (render: observations + frame ring;
+            # step: SURVEY 8(d) state bytes); the binding resource of both is VALU issue / latency
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": dk["achieved_gbs"], "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": dk["hbm_frac"], "traffic": dk["traffic_bytes_per_launch"],
+                         "bytes_per_env_step": dk["bytes_per_env_step"], "units_per_launch": n,
+                         "kernel_avg_ms": dk["ms"], "binding": "valu_issue_latency",
+                         "valu_issue_frac": dk["valu_issue_frac"], "wait_any_frac": dk["wait_any_frac"]},
+            "kernels": kernels,
             "kernel_ms_per_step": {"step_kernel": round(t_step_ms, 4), "reset_kernel": round(t_reset_ms, 4),
                                    "render_kernel": round(t_render_ms, 4), "timed_launches": n_timed},
             "env_errors": errors,
-            "gather": ({"bytes_per_rank_step": shard.layout.nbytes, "ranks": world,
-                        "received_bytes_per_rank_step": (world - 1) * shard.layout.nbytes} if gather else None),
+            "gather": ({"mode": args.gather_mode, "ranks": world, "bytes_per_rank_step": shard.layout.nbytes,
+                        "stacked_bytes_per_rank_step": shard.stacked_nbytes,
+                        "received_bytes_per_rank_step": (world - 1) * shard.layout.nbytes,
+                        "restack_bytes_per_rank_step": (world * n * restack_bytes(spec.preproc) if frames_only else 0)}
+                       if gather else None),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

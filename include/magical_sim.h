@@ -35,7 +35,8 @@ typedef struct {
     int32_t task;              /* 0 MoveToRegion 1 MoveToCorner 2 ClusterColour 3 ClusterShape 4 MatchRegions 5 MakeLine 6 FindDupe 7 FixColour 8 PickAndPlace */
     int32_t rand_flags;        /* bit 0 layout minor, 1 layout full, 2 colour, 3 shape type, 4 count, 5 dynamics,
                                   6 debug_reward (dense shaped reward: move_to_corner.py:85-100, pick_and_place.py:108-124) */
-    int32_t preproc;           /* 0 none, 1 LoRes4E, 2 LoResStack, 4 LoRes4A */
+    int32_t preproc;           /* 0 none, 1 LoRes4E (also LoResCHW4E / LoResCHW4A: same bytes), 2 LoResStack,
+                                  3 LoRes3EA, 4 LoRes4A (benchmarks/__init__.py:269-307) */
     int32_t num_envs;
     int32_t device;            /* HIP device ordinal */
     int32_t max_episode_steps; /* TimeLimit / BaseEnv.max_episode_steps */
@@ -56,6 +57,10 @@ typedef struct {
     double *eval_score;  /* f64[N] (info['eval_score']) */
     double *target;      /* PickAndPlace: f64[N,4] = (target_type, target_colour, target_position x, y)
                             (pick_and_place.py:87-107 observation extras), written at reset; NULL otherwise */
+    int32_t frames_only; /* 0: the preprocessor's outputs above.  1 (multi-GPU compact gather, magical_amd.dist):
+                            obs_allo / obs_ego receive only the current LoRes frame of each view, u8[N,96,96,3],
+                            for every LoRes preprocessor; obs_past is ignored and no frame stack or ring is kept
+                            (the receivers rebuild the stacks with mg_restack).  Switching modes needs a reset. */
 } mg_buffers;
 
 /* replaces gym.make(name) for N instances (benchmarks/__init__.py:232-266) */
@@ -105,6 +110,20 @@ int mg_set_episode_steps(mg_sim *sim, const int32_t *steps_dev, void *stream);
  * nframes "envs" (out_past NULL for LoResStack).  No mg_sim needed. */
 int mg_replay_lores(const uint8_t *frames, int32_t nframes, const int32_t *episode_start, int32_t preproc,
                     uint8_t *scratch, uint8_t *out_allo, uint8_t *out_ego, uint8_t *out_past, void *stream);
+/* Receiver side of the compact multi-GPU gather (magical_amd.dist.ShardedVecEnv): rebuilds the LoRes frame
+ * stacks (FlattenFrameStack / EagerDictFrameStack, benchmarks/__init__.py:51-147, reset frame filling every
+ * slot) of world * n envs from their all-gathered current frames.
+ * recv: device u8, `world` rank blocks of rank_stride bytes; block r holds env r*n+i's current allo frame
+ * u8[96,96,3] at off_allo + i*27648, its ego frame at off_ego + i*27648 and its done flag u8 at off_done + i
+ * (all offsets 16-byte aligned, as the frames-only outputs of mg_bind_outputs write them).
+ * ring: device u8[2][4][world*n][27648], caller-owned and persistent across calls (step t writes slot t % 4).
+ * all_fresh = 1 after a reset of every env; otherwise an env whose done flag is set restarts its stacks
+ * (auto-reset: its frame is the next episode's first).  Outputs for world*n envs, as mg_buffers' stacked
+ * outputs: preproc 1 (LoRes4E / CHW4E / CHW4A), 3 (LoRes3EA), 4 (LoRes4A): out_past u8[world*n,96,96,12]
+ * (allo / ego are the gathered frames themselves); 2 (LoResStack): out_allo, out_ego u8[world*n,96,96,12]. */
+int mg_restack(const uint8_t *recv, int32_t world, int32_t n, int64_t rank_stride, int64_t off_allo, int64_t off_ego,
+               int64_t off_done, int32_t preproc, int64_t step, int32_t all_fresh, uint8_t *ring, uint8_t *out_allo,
+               uint8_t *out_ego, uint8_t *out_past, void *stream);
 void mg_destroy(mg_sim *sim);
 const char *mg_last_error(void);
 

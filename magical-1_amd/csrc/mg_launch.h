@@ -13,7 +13,8 @@ struct RenderOut {
     uint8_t *obs_past;
     const uint8_t *mask;  // reset mask: envs with mask[e] == 0 are left untouched (null: all)
     int preproc;
-    int debug_skip;       // profiling builds only: 1 skip outlines, 2 skip fill, 4 skip HBM stores, 8 skip spans
+    int frames_only;      // 1: obs_allo / obs_ego get the current [N][96][96][3] frames only (no stacks, no ring)
+    int debug_skip;      // profiling builds only: 1 skip outlines, 2 skip fill, 4 skip HBM stores, 8 skip spans
     int small;            // 1: robot + arena + goal + one block at most (MoveToRegion, MoveToCorner) -> small LDS class
     int retry_in;         // set by mg_launch_render: render only the (env, view) pairs marked in S.rg_retry
     int retry_out;        // ... a pair this class cannot hold is marked for the next class (else an env error)

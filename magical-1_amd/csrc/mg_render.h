@@ -771,11 +771,14 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     const int head = S.hist_head[view * S.N + e];
     const int nh = fresh ? 0 : ((head + 1) & 3);
     const int pp = out.preproc;
-    const bool stacked = pp == MG_PREPROC_LORESSTACK || (pp == MG_PREPROC_LORES4E && view == 1) ||
-                         (pp == MG_PREPROC_LORES4A && view == 0);
-    const bool plain = pp != MG_PREPROC_LORESSTACK;   // the view's own current-frame output
+    // frames-only outputs (compact multi-GPU gather): the current frame of each view, no stacks, no ring
+    // (the receivers rebuild the stacks: mg_restack)
+    const bool fo = out.frames_only != 0;
+    const bool stacked = !fo && (pp == MG_PREPROC_LORESSTACK || (pp == MG_PREPROC_LORES4E && view == 1) ||
+                                 (pp == MG_PREPROC_LORES4A && view == 0));
+    const bool plain = fo || pp != MG_PREPROC_LORESSTACK;   // the view's own current-frame output
     // frame ring kept only where a stack reads it (LoRes3EA: ego ring, read by compose3ea_kernel)
-    const bool keep_ring = stacked || (pp == MG_PREPROC_LORES3EA && view == 1);
+    const bool keep_ring = stacked || (!fo && pp == MG_PREPROC_LORES3EA && view == 1);
     uint8_t *o_plain = view == 0 ? out.obs_allo : out.obs_ego;
     uint8_t *o_stack = pp == MG_PREPROC_LORESSTACK ? o_plain : out.obs_past;
     // 4x4 block of this thread: wave w covers block columns [32w, 32w + 32) of both block rows, so a

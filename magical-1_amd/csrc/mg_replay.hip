@@ -52,14 +52,9 @@ __global__ __launch_bounds__(256) void replay_downsample_kernel(const uint8_t *_
     dst[0] = o[0]; dst[1] = o[1]; dst[2] = o[2];
 }
 
-// pass 2: one thread per 4 pixels of one frame.  Stacked outputs concatenate, per pixel, the frames
-// oldest..newest (3 bytes each); src[k] is the workspace frame of stack slot k.
-__device__ __forceinline__ void stack4(const uint8_t *const src[4], size_t pix_off, uint8_t *dst) {
-    uint32_t f[4][3];
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-#pragma unroll
-        for (int w = 0; w < 3; w++) f[k][w] = ((const uint32_t *)(src[k] + pix_off))[w];
+// Stacked outputs concatenate, per pixel, the frames oldest..newest (3 bytes each): f[k] holds 4 pixels
+// (3 dwords) of stack slot k, written as 3 x 16 B.
+__device__ __forceinline__ void stack_regs(const uint32_t (&f)[4][3], uint8_t *dst) {
     uint4 *d = (uint4 *)dst;
 #pragma unroll
     for (int q = 0; q < 3; q++) {
@@ -72,6 +67,16 @@ __device__ __forceinline__ void stack4(const uint8_t *const src[4], size_t pix_o
         }
         d[q] = make_uint4(o[0], o[1], o[2], o[3]);
     }
+}
+
+// pass 2: one thread per 4 pixels of one frame; src[k] is the workspace frame of stack slot k.
+__device__ __forceinline__ void stack4(const uint8_t *const src[4], size_t pix_off, uint8_t *dst) {
+    uint32_t f[4][3];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int w = 0; w < 3; w++) f[k][w] = ((const uint32_t *)(src[k] + pix_off))[w];
+    stack_regs(f, dst);
 }
 
 __global__ __launch_bounds__(256) void replay_assemble_kernel(const uint8_t *__restrict__ lo,
@@ -109,6 +114,63 @@ __global__ __launch_bounds__(256) void replay_assemble_kernel(const uint8_t *__r
     }
     stack4(src, po, out_past + (size_t)f * LOFR * 4 + po * 4);
 }
+
+// Receiver-side frame stacks of the compact multi-GPU gather (mg_restack, magical_amd.dist): one thread per
+// 4 pixels of one env and one output stack (blockIdx.y: LoResStack 0 allo / 1 ego; else 0 = past_obs).
+// The ring view of the stack keeps the env's last 4 frames (slot t % 4 = this step); a fresh env (reset,
+// or done = auto-reset) fills every slot with its current frame, as the deques of
+// benchmarks/__init__.py:75-82,139-147 are filled at reset.  Byte work: per env and stack 12 B read (+ 36 B
+// of ring unless fresh), 12 B ring write and 48 B stacked output per 4 pixels -- HBM bound.
+__global__ __launch_bounds__(256) void restack_kernel(const uint8_t *__restrict__ recv, uint32_t world, uint32_t n,
+                                                      int64_t stride, int64_t off_a, int64_t off_e, int64_t off_d,
+                                                      int32_t preproc, uint32_t slot, int32_t all_fresh,
+                                                      uint8_t *__restrict__ ring, uint8_t *__restrict__ out0,
+                                                      uint8_t *__restrict__ out1) {
+    constexpr uint32_t Q = LO * LO / 4;
+    const uint32_t W = world * n;
+    const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t g = gid / Q, q = gid - g * Q;
+    if (g >= W) return;
+    const int s = blockIdx.y;
+    const uint32_t r = g / n, i = g - r * n;
+    const uint8_t *blk = recv + (size_t)r * stride;
+    const bool fresh = all_fresh || blk[off_d + i] != 0;
+    // the view this stack's frames come from (LoRes3EA: ego, with the current allo frame in slot 0)
+    const int rv = (preproc == MG_PREPROC_LORES4A || (preproc == MG_PREPROC_LORESSTACK && s == 0)) ? 0 : 1;
+    const size_t po = (size_t)q * 12;
+    const uint32_t *cur = (const uint32_t *)(blk + (rv ? off_e : off_a) + (size_t)i * LOFR + po);
+    uint8_t *rring = ring + (size_t)rv * 4 * W * LOFR;
+    auto rslot = [&](uint32_t sl) { return (uint32_t *)(rring + ((size_t)(sl & 3) * W + g) * LOFR + po); };
+    uint32_t f[4][3];
+#pragma unroll
+    for (int w = 0; w < 3; w++) f[3][w] = cur[w];
+    if (fresh) {
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+#pragma unroll
+            for (int w = 0; w < 3; w++) f[k][w] = f[3][w];
+#pragma unroll
+        for (uint32_t sl = 0; sl < 4; sl++) {
+            uint32_t *d = rslot(sl);
+            d[0] = f[3][0]; d[1] = f[3][1]; d[2] = f[3][2];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; k++) {          // stack slot k = frame t - (3 - k)
+            const uint32_t *src = rslot(slot + 1 + k);
+#pragma unroll
+            for (int w = 0; w < 3; w++) f[k][w] = src[w];
+        }
+        uint32_t *d = rslot(slot);
+        d[0] = f[3][0]; d[1] = f[3][1]; d[2] = f[3][2];
+    }
+    if (preproc == MG_PREPROC_LORES3EA) {      // allo depth 1 in front of the ego frames t-2, t-1, t
+        const uint32_t *a = (const uint32_t *)(blk + off_a + (size_t)i * LOFR + po);
+#pragma unroll
+        for (int w = 0; w < 3; w++) f[0][w] = a[w];
+    }
+    stack_regs(f, (s ? out1 : out0) + (size_t)g * LOFR * 4 + po * 4);
+}
 }  // namespace
 
 // launcher, C linkage (declared in mg_sim.hip next to the ABI entry mg_replay_lores)
@@ -124,5 +186,17 @@ extern "C" hipError_t mg_launch_replay(const uint8_t *frames, int32_t nframes, c
     const int64_t t2 = (int64_t)nframes * (LO * LO / 4);
     hipLaunchKernelGGL(replay_assemble_kernel, dim3((unsigned)((t2 + 255) / 256)), dim3(256), 0, st, scratch,
                        episode_start, nframes, preproc, out_allo, out_ego, out_past);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mg_launch_restack(const uint8_t *recv, int32_t world, int32_t n, int64_t stride, int64_t off_a,
+                                        int64_t off_e, int64_t off_d, int32_t preproc, int64_t step, int32_t all_fresh,
+                                        uint8_t *ring, uint8_t *out_allo, uint8_t *out_ego, uint8_t *out_past,
+                                        hipStream_t st) {
+    const int64_t t = (int64_t)world * n * (LO * LO / 4);
+    const bool two = preproc == MG_PREPROC_LORESSTACK;
+    hipLaunchKernelGGL(restack_kernel, dim3((unsigned)((t + 255) / 256), two ? 2 : 1), dim3(256), 0, st, recv,
+                       (uint32_t)world, (uint32_t)n, stride, off_a, off_e, off_d, preproc, (uint32_t)(step & 3),
+                       all_fresh, ring, two ? out_allo : out_past, out_ego);
     return hipGetLastError();
 }

@@ -326,7 +326,7 @@ MG_DEV void randomise_all(const MGState &S, const mg_library *L, int e, int lane
         }
         if (!failed) return;
     }
-    S.overflow[e] |= 2; // PlacementError after 10 retries
+    S.overflow[e] |= 2 | 64; // PlacementError after 10 retries (bit 2: this reset; bit 64: sticky, any reset)
 }
 
 // ---- tasks -----------------------------------------------------------------
@@ -427,6 +427,9 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
     const int lane = cfg.coop ? (int)(threadIdx.x & 63) : -1;
     const int f = cfg.flags;
     S.episode_steps[e] = 0;
+    // bit 2 reports the PlacementError of THIS reset (geom.py:335-336 raises out of reset(); the next reset
+    // draws a new layout from the advancing RNG), so it is cleared here; bit 64 keeps the history
+    S.overflow[e] &= ~2;
     for (int i = 0; i < MG_MAX_ARB; i++) { AT(S.akey, i) = -1; AT(S.acount, i) = 0; AT(S.astate, i) = ARB_FIRST; }
     S.nactive[e] = 0; S.stamp[e] = 0; S.curr_dt[e] = 0.0; S.nents[e] = 0; S.goal_ent[e] = -1;
     S.target_speed[e] = 0.0; S.rel_turn[e] = 0.0; S.target_finger[e] = 0.0;
@@ -555,7 +558,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
                 if (minor) lim = fmin(JITTER_POS_BOUND, lim);
                 shift_entity(S, e, query, v2(AT(S.ex, 1), AT(S.ey, 1)), AT(S.ba, AT(S.ebody0, query)));
                 if (randomise_pose(S, L, e, lane, query, true, lim, minor ? JITTER_ROT_BOUND : -1.0, 1u << 1) != 0)
-                    S.overflow[e] |= 2;
+                    S.overflow[e] |= 2 | 64;
             }
         }
     } else if (cfg.task == MG_TASK_FIX_COLOUR) { // fix_colour.py:67-176
@@ -608,7 +611,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
                     lim = lim > 0 ? lim : 0.0;
                     if (minor) lim = fmin(JITTER_POS_BOUND, lim);
                     if (randomise_pose(S, L, e, lane, 1 + nr + i, true, lim, minor ? JITTER_ROT_BOUND : -1.0, 1u << (1 + i)) != 0) {
-                        S.overflow[e] |= 2;
+                        S.overflow[e] |= 2 | 64;
                         break;
                     }
                 }

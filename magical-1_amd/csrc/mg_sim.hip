@@ -221,8 +221,9 @@ static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
 #endif
     ro.obs_allo = s->out.obs_allo; ro.obs_ego = s->out.obs_ego; ro.obs_past = s->out.obs_past;
     ro.preproc = s->preproc;
+    ro.frames_only = s->out.frames_only;
     HIPC(mg_launch_render(s->S, s->dlib, ro, 0, st));
-    if (s->preproc == MG_PREPROC_LORES3EA)
+    if (s->preproc == MG_PREPROC_LORES3EA && !s->out.frames_only)
         HIPC(mg_launch_compose3ea(s->S, (const uint8_t *)s->out.obs_allo, mask, (uint8_t *)s->out.obs_past, st));
     return 0;
 }
@@ -307,10 +308,13 @@ int mg_bind_outputs(mg_sim *s, const mg_buffers *b) {
     if (!s || !b) return set_err(-22, "mg_bind_outputs: null argument");
     if (s->preproc != MG_PREPROC_NONE && (!b->obs_allo || !b->obs_ego))
         return set_err(-22, "mg_bind_outputs: obs_allo / obs_ego required");
+    if (b->frames_only != 0 && b->frames_only != 1) return set_err(-22, "mg_bind_outputs: frames_only must be 0 or 1");
+    if (b->frames_only && s->preproc == MG_PREPROC_NONE)
+        return set_err(-22, "mg_bind_outputs: frames_only needs a LoRes preprocessor");
     if ((s->preproc == MG_PREPROC_LORES4E || s->preproc == MG_PREPROC_LORES4A || s->preproc == MG_PREPROC_LORES3EA) &&
-        !b->obs_past)
+        !b->frames_only && !b->obs_past)
         return set_err(-22, "mg_bind_outputs: obs_past required for this preprocessor");
-    const void *ptrs[3] = {b->obs_allo, b->obs_ego, b->obs_past};
+    const void *ptrs[3] = {b->obs_allo, b->obs_ego, b->frames_only ? nullptr : b->obs_past};
     for (const void *p : ptrs)
         if (((uintptr_t)p & 15) != 0) return set_err(-22, "mg_bind_outputs: observation buffers must be 16-byte aligned");
     if (s->task == MG_TASK_PICK_AND_PLACE && !b->target)
@@ -368,6 +372,38 @@ int mg_replay_lores(const uint8_t *frames, int32_t nframes, const int32_t *episo
         if (((uintptr_t)p & 15) != 0) return set_err(-22, "mg_replay_lores: buffers must be 16-byte aligned");
     HIPC(mg_launch_replay(frames, nframes, episode_start, preproc, scratch, out_allo, out_ego, out_past,
                           as_stream(stream)));
+    return 0;
+}
+
+hipError_t mg_launch_restack(const uint8_t *recv, int32_t world, int32_t n, int64_t stride, int64_t off_a,
+                             int64_t off_e, int64_t off_d, int32_t preproc, int64_t step, int32_t all_fresh,
+                             uint8_t *ring, uint8_t *out_allo, uint8_t *out_ego, uint8_t *out_past, hipStream_t st);
+
+int mg_restack(const uint8_t *recv, int32_t world, int32_t n, int64_t rank_stride, int64_t off_allo, int64_t off_ego,
+               int64_t off_done, int32_t preproc, int64_t step, int32_t all_fresh, uint8_t *ring, uint8_t *out_allo,
+               uint8_t *out_ego, uint8_t *out_past, void *stream) {
+    if (!recv || !ring || world <= 0 || n <= 0 || step < 0) return set_err(-22, "mg_restack: null argument or bad size");
+    const int64_t FR = (int64_t)MG_LORES * MG_LORES * 3;
+    if ((int64_t)world * n * (MG_LORES * MG_LORES / 4) >= ((int64_t)1 << 31))
+        return set_err(-22, "mg_restack: world * n too large for one launch");
+    if (preproc == MG_PREPROC_LORESSTACK) {
+        if (!out_allo || !out_ego) return set_err(-22, "mg_restack: LoResStack needs out_allo and out_ego");
+    } else if (preproc == MG_PREPROC_LORES4E || preproc == MG_PREPROC_LORES4A || preproc == MG_PREPROC_LORES3EA) {
+        if (!out_past) return set_err(-22, "mg_restack: out_past required for this preprocessor");
+    } else {
+        return set_err(-22, "mg_restack: preproc must be 1 (LoRes4E), 2 (LoResStack), 3 (LoRes3EA) or 4 (LoRes4A)");
+    }
+    if (off_allo < 0 || off_ego < 0 || off_done < 0 || off_allo + n * FR > rank_stride || off_ego + n * FR > rank_stride ||
+        off_done + n > rank_stride)
+        return set_err(-22, "mg_restack: a key of the rank block lies outside rank_stride");
+    const int64_t al[4] = {(int64_t)(uintptr_t)recv, rank_stride, off_allo, off_ego};
+    for (int64_t a : al)
+        if (a & 15) return set_err(-22, "mg_restack: recv, rank_stride and frame offsets must be 16-byte aligned");
+    const void *ptrs[4] = {ring, out_allo, out_ego, out_past};
+    for (const void *p : ptrs)
+        if (((uintptr_t)p & 15) != 0) return set_err(-22, "mg_restack: buffers must be 16-byte aligned");
+    HIPC(mg_launch_restack(recv, world, n, rank_stride, off_allo, off_ego, off_done, preproc, step, all_fresh, ring,
+                           out_allo, out_ego, out_past, as_stream(stream)));
     return 0;
 }
 

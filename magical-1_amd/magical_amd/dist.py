@@ -6,17 +6,27 @@ with W * n envs would run.  Instances are independent,
 so stepping needs no collective.  The north star's exchange -- every rank gets
 the whole node's step results -- is one all-gather per step:
 
-* each rank's step outputs (observations, reward, done, eval_score[, target])
-  live in ONE packed u8 buffer (PackedLayout): the simulator writes straight
-  into its key views (VecMagicalEnv.bind_outputs), so there is no pack copy;
+* each rank's step outputs live in ONE packed u8 buffer (PackedLayout): the
+  simulator writes straight into its key views (VecMagicalEnv.bind_outputs),
+  so there is no pack copy;
 * one ``all_gather_into_tensor`` of that buffer (RCCL over xGMI with the
   "nccl" process group, gloo for CPU tensors in the tests) yields [W, bytes];
-  PackedLayout.unpack turns it into per-key [W, n, ...] views, again without
-  a copy (global env id = r * n + i);
-* two such buffers alternate between steps and the collective runs on its own
-  HIP stream, so the gather of step t overlaps the compute of step t + 1
-  (ShardedVecEnv.step_async).  A step's gathered views stay valid until the
-  step after next.
+  PackedLayout.unpack turns it into per-key [W, n, ...] views without a copy
+  (global env id = r * n + i);
+* gather_mode "frames" (default): the packed buffer holds only the CURRENT
+  LoRes frame of each view plus reward / done / eval_score[, target] -- 55 312
+  B per env instead of 165 904 (LoRes4E) or 221 200 (LoResStack) -- because 3
+  of every 4 stacked frames already reached every rank in earlier steps.  Each
+  receiver rebuilds the frame stacks of all W * n envs from a ring of their
+  last 4 frames (mg_restack, a HIP kernel; the reset frame fills every slot as
+  in benchmarks/__init__.py:75-82,139-147, and an env whose done flag is set
+  restarts its stacks: its frame is the next episode's first).  The simulator
+  binds its outputs in frames-only mode, so it writes no stacks of its own.
+  gather_mode "stacked" gathers the preprocessor's whole outputs instead;
+* two buffer sets alternate between steps and the collective (then the
+  restack) runs on its own HIP stream, so the exchange of step t overlaps the
+  compute of step t + 1 (ShardedVecEnv.step_async).  A step's gathered views
+  stay valid until the step after next.
 """
 import collections
 
@@ -25,6 +35,7 @@ import torch
 import torch.distributed as dist
 
 _ALIGN = 256  # byte alignment of every key inside the packed buffer (the simulator needs 16)
+LOFR = 96 * 96 * 3  # bytes of one LoRes RGB frame
 
 
 def shard_range(envs_per_rank, rank):
@@ -50,6 +61,15 @@ def all_gather_batch(tensors, group=None):
     return out
 
 
+# mg_restack / mg_bind_outputs preprocessor ids (include/magical_sim.h)
+GPU_PREPROC = {"LoRes4E": 1, "LoResCHW4E": 1, "LoResCHW4A": 1, "LoResStack": 2, "LoRes3EA": 3, "LoRes4A": 4}
+
+
+def stacked_keys(preproc):
+    """Keys whose values are 4-frame stacks (rebuilt on the receivers in gather_mode 'frames')."""
+    return ("allo", "ego") if preproc == "LoResStack" else ("past_obs",)
+
+
 class PackedLayout:
     """Byte layout of one rank's step outputs in a single u8 buffer: per key a contiguous [n, ...]
     block at a 256-byte aligned offset, in the order of `fields` (name, per-env shape, dtype)."""
@@ -64,24 +84,35 @@ class PackedLayout:
             self.fields.append((name, shape, dtype, off, nb))
             off = (off + nb + _ALIGN - 1) // _ALIGN * _ALIGN
         self.nbytes = off
+        self.chw = False
+        self.frames_only = False
 
     @classmethod
-    def for_spec(cls, spec, n):
-        """The fields VecMagicalEnv.output_buffers() binds for a registry spec (raw HWC observations)."""
+    def for_spec(cls, spec, n, frames_only=False):
+        """The fields VecMagicalEnv.output_buffers() binds for a registry spec (raw HWC observations);
+        frames_only: the current frame of each view instead of the preprocessor's stacks."""
         from . import registry
         from .envs import _obs_shapes
         if spec.preproc is None:
             raise ValueError("packed gather: the unwrapped 384^2 view is rendered on demand, not bound")
         chw = registry.PREPROCESSORS[spec.preproc].get("channels_first", False)
         fields = []
-        for k, s in _obs_shapes(spec).items():
-            fields.append((k, (s[1], s[2], s[0]) if chw else s, torch.uint8))   # buffers are HWC
+        if frames_only:
+            fields += [("allo", (96, 96, 3), torch.uint8), ("ego", (96, 96, 3), torch.uint8)]
+        else:
+            for k, s in _obs_shapes(spec).items():
+                fields.append((k, (s[1], s[2], s[0]) if chw else s, torch.uint8))   # buffers are HWC
         fields += [("reward", (), torch.float32), ("done", (), torch.bool), ("eval_score", (), torch.float64)]
         if spec.task == "PickAndPlace":
             fields.append(("target", (4,), torch.float64))
         lay = cls(n, fields)
         lay.chw = chw
+        lay.frames_only = frames_only
+        lay.preproc = spec.preproc
         return lay
+
+    def offset(self, name):
+        return next(f[3] for f in self.fields if f[0] == name)
 
     def views(self, buf):
         """Per-key [n, ...] views into one rank's packed buffer (u8, nbytes)."""
@@ -101,82 +132,150 @@ class PackedLayout:
         return out
 
 
-class GatheredStep:
-    """Handle of one step's packed all-gather: wait() orders the caller's current stream after it."""
+class NativeRestacker:
+    """Receiver-side frame stacks of the frames-only gather on the GPU (mg_restack): keeps a ring of the
+    last 4 frames of each view for all W * n envs, u8[2][4][W * n][96 * 96 * 3]."""
 
-    def __init__(self, layout, recv, work):
-        self.layout, self.recv, self.work = layout, recv, work
+    def __init__(self, layout, world, device):
+        from . import native
+        self.lib, self.native = native.load(), native
+        self.layout, self.world = layout, world
+        self.preproc = GPU_PREPROC[layout.preproc]
+        self.ring = torch.empty(2 * 4 * world * layout.n * LOFR, dtype=torch.uint8, device=device)
+        self.off = (layout.offset("allo"), layout.offset("ego"), layout.offset("done"))
+
+    def __call__(self, recv, outs, step, all_fresh):
+        import ctypes
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        st = ctypes.c_void_p(torch.cuda.current_stream(recv.device).cuda_stream)
+        self.native.check(self.lib.mg_restack(
+            p(recv), self.world, self.layout.n, self.layout.nbytes, self.off[0], self.off[1], self.off[2],
+            self.preproc, int(step), 1 if all_fresh else 0, p(self.ring), p(outs.get("allo")), p(outs.get("ego")),
+            p(outs.get("past_obs")), st))
+
+
+class GatheredStep:
+    """Handle of one step's exchange: wait() orders the caller's current stream after it (the all-gather
+    and, in gather_mode 'frames', the receiver-side restack)."""
+
+    def __init__(self, layout, recv, stacks, work=None, event=None):
+        self.layout, self.recv, self.stacks, self.work, self.event = layout, recv, stacks, work, event
 
     def wait(self):
         if self.work is not None:
             self.work.wait()
             self.work = None
+        if self.event is not None:
+            torch.cuda.current_stream(self.recv.device).wait_event(self.event)
         return self
 
     def results(self):
-        """(obs dict of [W, n, ...] observation views, reward, done, info={'eval_score'[, 'target']}), all [W, n...]"""
+        """(obs dict of [W, n, ...] observation views, reward, done, info={'eval_score'[, 'target']}), all [W, n...]:
+        observation keys and order as VecMagicalEnv returns them (PickAndPlace: allo, ego, target_type,
+        target_colour, target_position[, past_obs])."""
         self.wait()
         v = self.layout.unpack(self.recv)
-        if getattr(self.layout, "chw", False):   # as VecMagicalEnv returns them: channels-first views
+        world, n = v["reward"].shape
+        for k, t in (self.stacks or {}).items():   # rebuilt frame stacks replace / add their keys
+            v[k] = t.view(world, n, 96, 96, 12)
+        if self.layout.chw:   # as VecMagicalEnv returns them: channels-first views
             for k in [k for k in v if v[k].dim() == 5]:
                 v[k] = v[k].permute(0, 1, 4, 2, 3)
         info = {"eval_score": v.pop("eval_score")}
-        if "target" in v:
-            info["target"] = v.pop("target")
         rew, done = v.pop("reward"), v.pop("done")
-        return v, rew, done, info
+        obs = collections.OrderedDict([("allo", v.pop("allo")), ("ego", v.pop("ego"))])
+        if "target" in v:
+            t = info["target"] = v.pop("target")
+            t32 = t.to(torch.float32)
+            obs["target_type"], obs["target_colour"], obs["target_position"] = t32[..., 0:1], t32[..., 1:2], t32[..., 2:4]
+        if "past_obs" in v:
+            obs["past_obs"] = v.pop("past_obs")
+        return obs, rew, done, info
 
 
 class ShardedVecEnv:
     """This rank's shard of a node-wide batch of envs (VecMagicalEnv underneath).
 
-    gather=True: every step's results of all ranks are all-gathered to every rank through one packed
-    buffer (see the module docstring); step() returns the gathered [W, n, ...] views, step_async() the
-    handle without waiting, so the collective of step t overlaps step t + 1."""
+    gather=True: every step's results of all ranks reach every rank (see the module docstring); step()
+    returns the gathered [W, n, ...] views, step_async() the handle without waiting, so the exchange of
+    step t overlaps step t + 1.  gather_mode 'frames' (default) all-gathers only the current frames and
+    rebuilds the stacks on each receiver (`restacker`: NativeRestacker on the GPU; CPU tensors need one
+    passed in -- the gloo tests use the oracle's); 'stacked' all-gathers the whole observations."""
 
-    def __init__(self, env_name, envs_per_rank, rank=None, device=None, base_seed=1000, gather=False, vec=None):
+    def __init__(self, env_name, envs_per_rank, rank=None, device=None, base_seed=1000, gather=False, vec=None,
+                 gather_mode="frames", restacker=None, max_episode_steps=None):
         from . import registry
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.envs_per_rank = envs_per_rank
         self.gather = gather
+        spec = registry.lookup(env_name)
         if vec is None:
             from .envs import VecMagicalEnv
             vec = VecMagicalEnv(env_name, envs_per_rank, device=device or f"cuda:{torch.cuda.current_device()}",
-                                seeds=shard_seeds(envs_per_rank, self.rank, base_seed))
+                                seeds=shard_seeds(envs_per_rank, self.rank, base_seed),
+                                max_episode_steps=max_episode_steps)
         self.vec = vec
         if gather:
-            self.layout = PackedLayout.for_spec(registry.lookup(env_name), envs_per_rank)
+            if gather_mode not in ("frames", "stacked"):
+                raise ValueError(f"gather_mode must be 'frames' or 'stacked', not {gather_mode!r}")
+            self.gather_mode = gather_mode
+            frames = gather_mode == "frames"
+            self.layout = PackedLayout.for_spec(spec, envs_per_rank, frames_only=frames)
+            self.stacked_nbytes = PackedLayout.for_spec(spec, envs_per_rank).nbytes
             dev = torch.device(device) if device is not None else getattr(vec, "device", torch.device("cpu"))
             self.device = dev
             self.send = [torch.empty(self.layout.nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
             self.recv = [torch.empty(self.world * self.layout.nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self.stacks = [None, None]
+            if frames:
+                wn = self.world * envs_per_rank
+                self.stacks = [collections.OrderedDict((k, torch.empty((wn, 96, 96, 12), dtype=torch.uint8, device=dev))
+                                                       for k in stacked_keys(spec.preproc)) for _ in range(2)]
+                if restacker is None:
+                    if dev.type != "cuda":
+                        raise ValueError("gather_mode 'frames' on CPU tensors needs a restacker")
+                    restacker = NativeRestacker(self.layout, self.world, dev)
+            self.restacker = restacker
             self.pending = [None, None]
             self.comm_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
             self.t = 0
 
     # -- packed gather pipeline ---------------------------------------------------------------------------
     def _begin(self):
-        """Buffer of this step: the gather that last read it (two steps ago) must be done first."""
+        """Buffer set of this step: the exchange that last used it (two steps ago) must be done first."""
         b = self.t % 2
         if self.pending[b] is not None:
             self.pending[b].wait()
             self.pending[b] = None
-        self.vec.bind_outputs(self.layout.views(self.send[b]))
+        self.vec.bind_outputs(self.layout.views(self.send[b]), frames_only=self.layout.frames_only)
         return b
 
-    def _launch(self, b):
-        send, recv = self.send[b], self.recv[b]
+    def _finish_outputs(self, b):
+        # PickAndPlace's target is written by the simulator only at reset: copy the env's persistent
+        # buffer into this step's packed views (ADVICE r2: never gather a stale or unwritten target)
+        if self.layout.fields[-1][0] == "target":
+            self.layout.views(self.send[b])["target"].copy_(self.vec.target)
+
+    def _launch(self, b, all_fresh):
+        send, recv, stacks = self.send[b], self.recv[b], self.stacks[b]
+        step = self.t
         if self.comm_stream is not None:
             ev = torch.cuda.current_stream(self.device).record_event()
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
                 work = dist.all_gather_into_tensor(recv, send, async_op=True)
-                send.record_stream(self.comm_stream)
-                recv.record_stream(self.comm_stream)
+                work.wait()   # the side stream (not the host) waits for the collective
+                if stacks is not None:
+                    self.restacker(recv, stacks, step, all_fresh)
+                done_ev = self.comm_stream.record_event()
+            h = GatheredStep(self.layout, recv, stacks, event=done_ev)
         else:
             work = dist.all_gather_into_tensor(recv, send, async_op=True)
-        h = GatheredStep(self.layout, recv, work)
+            work.wait()
+            if stacks is not None:
+                self.restacker(recv, stacks, step, all_fresh)
+            h = GatheredStep(self.layout, recv, stacks)
         self.pending[b] = h
         self.t += 1
         return h
@@ -184,12 +283,14 @@ class ShardedVecEnv:
     def reset_async(self):
         b = self._begin()
         self.vec.reset()
-        return self._launch(b)
+        self._finish_outputs(b)
+        return self._launch(b, all_fresh=True)
 
     def step_async(self, actions):
         b = self._begin()
         self.vec.step(actions)
-        return self._launch(b)
+        self._finish_outputs(b)
+        return self._launch(b, all_fresh=False)
 
     # -- gym-style ------------------------------------------------------------------------------------------
     def reset(self):
@@ -202,8 +303,11 @@ class ShardedVecEnv:
             return self.step_async(actions).results()
         return self.vec.step(actions)
 
-    def close(self):
+    def wait_all(self):
         for h in getattr(self, "pending", []):
             if h is not None:
                 h.wait()
+
+    def close(self):
+        self.wait_all()
         self.vec.close()

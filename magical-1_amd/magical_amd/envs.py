@@ -8,8 +8,9 @@
   BaseEnv + preprocessors (base_env.py:190-351, benchmarks/__init__.py:51-190):
   numpy observations, done at max_episode_steps, explicit reset().
 
-Observation buffers returned by VecMagicalEnv are the simulator's output
-tensors; they are rewritten by the next step (copy them to keep them).
+Every tensor VecMagicalEnv.reset()/step() returns (observations, reward, done,
+info values) is one of the simulator's bound output buffers: it is valid until
+the next reset()/step() rewrites it (clone it to keep it).
 """
 import collections
 import ctypes
@@ -116,6 +117,7 @@ class VecMagicalEnv:
         self.done = torch.zeros(n, dtype=torch.bool, device=dev)  # the C ABI writes u8 0/1: same bytes
         self.eval_score = torch.zeros(n, dtype=torch.float64, device=dev)
         self.target = torch.zeros((n, 4), dtype=torch.float64, device=dev) if self.spec.task == "PickAndPlace" else None
+        self.frames_only = False
         self._bind()
         self.action_space = spaces.Discrete(18)
         self.observation_space = observation_space(self.spec)
@@ -127,17 +129,22 @@ class VecMagicalEnv:
         buf.obs_allo, buf.obs_ego, buf.obs_past = ptr(self.obs_allo), ptr(self.obs_ego), ptr(self.obs_past)
         buf.reward, buf.done, buf.eval_score = ptr(self.reward), ptr(self.done), ptr(self.eval_score)
         buf.target = ptr(self.target)
+        buf.frames_only = 1 if self.frames_only else 0
         native.check(self.lib.mg_bind_outputs(self.handle, ctypes.byref(buf)))
 
-    def bind_outputs(self, views):
+    def bind_outputs(self, views, frames_only=False):
         """Write the following steps' outputs into caller-owned device tensors (e.g. views into one packed
-        buffer per step, magical_amd.dist.PackedLayout): keys as output_buffers()."""
+        buffer per step, magical_amd.dist.PackedLayout): keys as output_buffers().  frames_only: 'allo' /
+        'ego' receive only the current [n, 96, 96, 3] frames for every LoRes preprocessor (no stacks;
+        magical_amd.dist's compact gather restacks on the receivers) -- changing the mode needs a reset.
+        PickAndPlace's target stays in the env's own persistent buffer (the simulator writes it only at
+        reset); callers copy it where they need it."""
         if self.spec.preproc is None:
             raise ValueError("bind_outputs: the unwrapped 384^2 view is rendered on demand, not bound")
         self.obs_allo, self.obs_ego = views["allo"], views["ego"]
-        self.obs_past = views.get("past_obs")
+        self.obs_past = None if frames_only else views.get("past_obs")
         self.reward, self.done, self.eval_score = views["reward"], views["done"], views["eval_score"]
-        self.target = views.get("target")
+        self.frames_only = bool(frames_only)
         self._bind()
 
     def output_buffers(self):

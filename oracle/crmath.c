@@ -110,7 +110,7 @@ static dd kcos(dd r) {
     return p;
 }
 
-double o_crsin(double x) {
+static double cr_sin(double x) {
     if (fabs(x) < 1.4901161193847656e-08) return x; /* |x| < 2^-26: sin x rounds to x */
     int q; dd r, v;
     reduce(x, &q, &r);
@@ -123,7 +123,7 @@ double o_crsin(double x) {
     return v.hi + v.lo;
 }
 
-double o_crcos(double x) {
+static double cr_cos(double x) {
     if (fabs(x) < 7.450580596923828e-09) return 1.0; /* |x| < 2^-27 */
     int q; dd r, v;
     reduce(x, &q, &r);
@@ -153,7 +153,7 @@ static dd dd_div(dd a, dd b) {
 
 /* math.tan (geom.py:22 regular_poly_circ_rad_to_side_length): sin/cos in
  * double-double, one division, rounded once */
-double o_crtan(double x) {
+static double cr_tan(double x) {
     if (fabs(x) < 1.4901161193847656e-08) return x;
     int q; dd r, s, c;
     reduce(x, &q, &r);
@@ -167,3 +167,15 @@ double o_crtan(double x) {
     dd t = dd_div(s, c);
     return t.hi + t.lo;
 }
+
+/* the exported functions: correctly rounded, or this image's libm in the measurement build
+ * (make libm -> _build/libmg_oracle_libm.so, tools/libm_vs_cr.py) */
+#ifdef ORACLE_LIBM_TRIG
+double o_crsin(double x) { return sin(x); }
+double o_crcos(double x) { return cos(x); }
+double o_crtan(double x) { return tan(x); }
+#else
+double o_crsin(double x) { return cr_sin(x); }
+double o_crcos(double x) { return cr_cos(x); }
+double o_crtan(double x) { return cr_tan(x); }
+#endif

@@ -111,6 +111,12 @@ void o_palette(uint8_t out[5][4][3]);
 /* cv2 INTER_AREA 384^2 -> 96^2 restatement on an arbitrary frame */
 void o_downsample(const uint8_t *frame384, uint8_t *out96);
 
+/* pure restatements of the reference's scorers / action decode on explicit inputs (reference-fixture tests) */
+double o_score_move_to_corner(double rx, double ry);                         /* move_to_corner.py:67-77 */
+double o_shaped_move_to_corner(double rx, double ry, double sx, double sy);   /* move_to_corner.py:86-100 */
+double o_cluster_score(int nblocks, const int *val, const double *x, const double *y); /* cluster.py:166-216 */
+void o_action_decode(int action, double out[3]);                              /* entities.py:148-190,435-453 */
+
 #ifdef __cplusplus
 }
 #endif

@@ -12,7 +12,9 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libmg_oracle.so")
+# MG_ORACLE_TRIG=libm: the measurement build with this image's libm sin/cos (tools/libm_vs_cr.py)
+_LIBM = os.environ.get("MG_ORACLE_TRIG") == "libm"
+LIB_PATH = os.path.join(HERE, "_build", "libmg_oracle_libm.so" if _LIBM else "libmg_oracle.so")
 
 TASKS = {"MoveToRegion": 0, "MoveToCorner": 1, "ClusterColour": 2, "ClusterShape": 3, "MatchRegions": 4,
          "MakeLine": 5, "FindDupe": 6, "FixColour": 7, "PickAndPlace": 8}
@@ -22,7 +24,7 @@ _lib = None
 
 
 def build():
-    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    subprocess.run(["make", "-s", "-C", HERE] + (["libm"] if _LIBM else []), check=True)
 
 
 def lib():
@@ -204,4 +206,105 @@ def downsample(frame):
     assert frame.shape == (384, 384, 3)
     out = np.zeros((96, 96, 3), dtype=np.uint8)
     lib().o_downsample(ptr(frame), ptr(out))
+    return out
+
+
+class OracleRestacker:
+    """Reference frame-stack rule over an all-gathered frames-only batch (TEST INFRASTRUCTURE: the CPU
+    counterpart of mg_restack that the gloo tests hand to magical_amd.dist.ShardedVecEnv).
+
+    Restates benchmarks/__init__.py:51-147 per env: EagerDictFrameStack / FlattenFrameStack keep a deque of
+    the last `depth` frames, filled with the reset frame at reset (:75-82, :139-147); under SB3's
+    DummyVecEnv auto-reset the frame returned with done is the next episode's reset frame.  Stacks are
+    the frames oldest..newest concatenated on the channel axis; LoRes3EA puts the current allo frame in
+    front of the last 3 ego frames (allo depth 1, ego depth 3)."""
+
+    def __init__(self, layout, preproc):
+        self.layout, self.pp = layout, preproc
+        self.deq = {}
+
+    def __call__(self, recv, outs, step, all_fresh):
+        v = self.layout.unpack(recv)
+        W, n = v["done"].shape
+        done = v["done"].reshape(-1).numpy().astype(bool)
+        cur = {k: v[k].reshape(W * n, 96, 96, 3).numpy() for k in ("allo", "ego")}
+        for k, c in cur.items():
+            if all_fresh or k not in self.deq:
+                d = np.repeat(c[:, None], 4, axis=1)
+            else:
+                d = np.concatenate([self.deq[k][:, 1:], c[:, None]], axis=1)
+                d[done] = c[done][:, None]
+            self.deq[k] = d
+        cat = lambda frames: np.concatenate(frames, axis=-1)  # noqa: E731
+        res = {}
+        if self.pp == "LoResStack":
+            res["allo"] = cat([self.deq["allo"][:, k] for k in range(4)])
+            res["ego"] = cat([self.deq["ego"][:, k] for k in range(4)])
+        elif self.pp == "LoRes4A":
+            res["past_obs"] = cat([self.deq["allo"][:, k] for k in range(4)])
+        elif self.pp == "LoRes3EA":
+            res["past_obs"] = cat([cur["allo"]] + [self.deq["ego"][:, k] for k in range(1, 4)])
+        else:   # LoRes4E, LoResCHW4E, LoResCHW4A
+            res["past_obs"] = cat([self.deq["ego"][:, k] for k in range(4)])
+        import torch
+        for k, a in res.items():
+            outs[k].copy_(torch.from_numpy(a))
+
+
+def _pure():
+    L = lib()
+    if not getattr(L, "_pure_set", False):
+        d, i, vp = ctypes.c_double, ctypes.c_int, ctypes.c_void_p
+        L.o_score_move_to_corner.restype = d; L.o_score_move_to_corner.argtypes = [d, d]
+        L.o_shaped_move_to_corner.restype = d; L.o_shaped_move_to_corner.argtypes = [d, d, d, d]
+        L.o_cluster_score.restype = d; L.o_cluster_score.argtypes = [i, vp, vp, vp]
+        L.o_action_decode.restype = None; L.o_action_decode.argtypes = [i, vp]
+        L._pure_set = True
+    return L
+
+
+def score_move_to_corner(rx, ry):
+    return _pure().o_score_move_to_corner(float(rx), float(ry))
+
+
+def shaped_move_to_corner(rx, ry, sx, sy):
+    return _pure().o_shaped_move_to_corner(float(rx), float(ry), float(sx), float(sy))
+
+
+def cluster_score(vals, xy):
+    """vals: per block the rank of its characteristic value among the values present; xy: [n, 2]"""
+    v = np.ascontiguousarray(vals, dtype=np.int32)
+    xy = np.asarray(xy, dtype=np.float64)
+    x, y = np.ascontiguousarray(xy[:, 0]), np.ascontiguousarray(xy[:, 1])
+    return _pure().o_cluster_score(len(v), ptr(v), ptr(x), ptr(y))
+
+
+def action_decode(action):
+    out = np.zeros(3)
+    _pure().o_action_decode(int(action), ptr(out))
+    return out
+
+
+def stack_lores(lo, starts, preproc, channels_first=False):
+    """Per-frame LoRes observation dicts from per-frame downsampled (allo, ego) frames by the reference
+    wrappers' rules (benchmarks/__init__.py:51-147,232-307): frame f's stacks reach back to the first frame
+    of its episode, starts[f] (the reset frame fills every deque slot)."""
+    import collections
+    out = []
+    for f in range(len(lo)):
+        back = lambda k: max(f - k, starts[f])  # noqa: E731
+        if preproc == "LoResStack":
+            out.append(collections.OrderedDict(
+                (k, np.concatenate([lo[back(j)][v] for j in (3, 2, 1, 0)], axis=-1)) for v, k in enumerate(("allo", "ego"))))
+            continue
+        if preproc == "LoRes3EA":
+            frames = [lo[f][0]] + [lo[back(j)][1] for j in (2, 1, 0)]
+        elif preproc == "LoRes4A":
+            frames = [lo[back(j)][0] for j in (3, 2, 1, 0)]
+        else:
+            frames = [lo[back(j)][1] for j in (3, 2, 1, 0)]
+        d = collections.OrderedDict([("allo", lo[f][0]), ("ego", lo[f][1]), ("past_obs", np.concatenate(frames, -1))])
+        if channels_first:
+            d = collections.OrderedDict((k, np.moveaxis(v, -1, 0)) for k, v in d.items())
+        out.append(d)
     return out

@@ -11,6 +11,7 @@
  * Transform); style.py (palette).
  */
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #include <float.h>
 #include "oscene.h"
@@ -1117,6 +1118,14 @@ void oscene_set_action(OEnv *e, int action) {
     else if (flags & 32) e->target_finger = -0.0;
 }
 
+/* the decoded control targets of one action (target_speed, rel_turn_angle, target_finger_angle) */
+void o_action_decode(int action, double out[3]) {
+    OEnv *e = (OEnv *)calloc(1, sizeof(OEnv));
+    oscene_set_action(e, action);
+    out[0] = e->target_speed; out[1] = e->rel_turn; out[2] = e->target_finger;
+    free(e);
+}
+
 void oscene_robot_update(OEnv *e) {
     OEntity *r = &e->ents[e->robot];
     OSpace *s = &e->space;
@@ -1174,9 +1183,9 @@ static double score_move_to_region(OEnv *e) {
     return dist <= 0 ? 1.0 : 0.0;
 }
 
-static double score_move_to_corner(OEnv *e) {
-    vec2 p = e->space.bodies[e->ents[e->robot].body0].p;
-    double dx = -1.0 - p.x, dy = 1.0 - p.y;
+/* move_to_corner.py:67-77: the ROBOT's distance to the top-left corner (fork quirk: not the block's) */
+double o_score_move_to_corner(double rx, double ry) {
+    double dx = -1.0 - rx, dy = 1.0 - ry;
     double dist = sqrt(fma(dy, dy, dx * dx)); /* np.linalg.norm -> BLAS ddot */
     double succeed = sqrt(2.0) / 2, furthest = sqrt(2.0);
     double drange = furthest - succeed;
@@ -1185,41 +1194,36 @@ static double score_move_to_corner(OEnv *e) {
     return score < 1.0 ? score : 1.0;
 }
 
-static double score_cluster(OEnv *e, int by_type) {
-    /* characteristic values: np.unique sorts the str-enum values */
-    static const int COLOUR_ORDER[4] = {COL_BLUE, COL_GREEN, COL_RED, COL_YELLOW};
-    static const int TYPE_ORDER[4] = {SHAPE_CIRCLE, SHAPE_PENTAGON, SHAPE_SQUARE, SHAPE_STAR};
-    const int *order = by_type ? TYPE_ORDER : COLOUR_ORDER;
-    int vals[4], nvals = 0;
-    for (int k = 0; k < 4; k++) {
-        for (int i = 0; i < e->nents; i++) {
-            OEntity *en = &e->ents[i];
-            if (en->kind != ENT_BLOCK) continue;
-            if ((by_type ? en->type : en->colour) == order[k]) { vals[nvals++] = order[k]; break; }
-        }
-    }
+static double score_move_to_corner(OEnv *e) {
+    vec2 p = e->space.bodies[e->ents[e->robot].body0].p;
+    return o_score_move_to_corner(p.x, p.y);
+}
+
+/* cluster.py:166-216 on block positions: val[i] = the rank of block i's characteristic value among the
+ * values present (np.unique order), blocks in entity (insertion) order */
+double o_cluster_score(int nblocks, const int *val, const double *x, const double *y) {
+    int present[4] = {0, 0, 0, 0};
+    for (int i = 0; i < nblocks; i++) present[val[i]] = 1;
+    int nvals = 0;
+    for (int k = 0; k < 4; k++) nvals += present[k];
     double cx[4], cy[4];
     for (int c = 0; c < nvals; c++) {
         double sx = 0, sy = 0; int cnt = 0;
-        for (int i = 0; i < e->nents; i++) {
-            OEntity *en = &e->ents[i];
-            if (en->kind != ENT_BLOCK || (by_type ? en->type : en->colour) != vals[c]) continue;
-            vec2 p = e->space.bodies[en->body0].p;
-            if (cnt == 0) { sx = p.x; sy = p.y; } else { sx += p.x; sy += p.y; }
+        for (int i = 0; i < nblocks; i++) {
+            if (val[i] != c) continue;
+            if (cnt == 0) { sx = x[i]; sy = y[i]; } else { sx += x[i]; sy += y[i]; }
             cnt++;
         }
         cx[c] = sx / cnt; cy[c] = sy / cnt;
     }
     int n_blocks = 0, n_correct = 0;
     for (int c = 0; c < nvals; c++) {
-        for (int i = 0; i < e->nents; i++) {
-            OEntity *en = &e->ents[i];
-            if (en->kind != ENT_BLOCK || (by_type ? en->type : en->colour) != vals[c]) continue;
+        for (int i = 0; i < nblocks; i++) {
+            if (val[i] != c) continue;
             n_blocks++;
-            vec2 p = e->space.bodies[en->body0].p;
             double sse[4];
             for (int k = 0; k < nvals; k++) {
-                double dx = p.x - cx[k], dy = p.y - cy[k];
+                double dx = x[i] - cx[k], dy = y[i] - cy[k];
                 sse[k] = dx * dx + dy * dy;
             }
             double true_sse = sse[c], nearest_bad = INFINITY;
@@ -1231,6 +1235,34 @@ static double score_cluster(OEnv *e, int by_type) {
     double frac = (double)n_correct / (n_blocks > 1 ? n_blocks : 1);
     double v = frac - 0.75;
     return (v > 0 ? v : 0) / (1 - 0.75);
+}
+
+static double score_cluster(OEnv *e, int by_type) {
+    /* characteristic values: np.unique sorts the str-enum values */
+    static const int COLOUR_ORDER[4] = {COL_BLUE, COL_GREEN, COL_RED, COL_YELLOW};
+    static const int TYPE_ORDER[4] = {SHAPE_CIRCLE, SHAPE_PENTAGON, SHAPE_SQUARE, SHAPE_STAR};
+    const int *order = by_type ? TYPE_ORDER : COLOUR_ORDER;
+    int rank_of[4] = {-1, -1, -1, -1}, nvals = 0;
+    for (int k = 0; k < 4; k++) {
+        for (int i = 0; i < e->nents; i++) {
+            OEntity *en = &e->ents[i];
+            if (en->kind != ENT_BLOCK) continue;
+            if ((by_type ? en->type : en->colour) == order[k]) { rank_of[k] = nvals++; break; }
+        }
+    }
+    int val[O_MAX_ENTS], nb = 0;
+    double x[O_MAX_ENTS], y[O_MAX_ENTS];
+    for (int i = 0; i < e->nents; i++) {
+        OEntity *en = &e->ents[i];
+        if (en->kind != ENT_BLOCK) continue;
+        const int v = by_type ? en->type : en->colour;
+        int k = 0;
+        while (order[k] != v) k++;
+        val[nb] = rank_of[k];
+        x[nb] = e->space.bodies[en->body0].p.x; y[nb] = e->space.bodies[en->body0].p.y;
+        nb++;
+    }
+    return o_cluster_score(nb, val, x, y);
 }
 
 /* entities.py:803-863 get_overlapping_ents(com_overlap=True) of goal entity gi over the block
@@ -1397,10 +1429,15 @@ double oscene_debug_reward(OEnv *e) {
     int shape = -1; /* MoveToCorner: the block */
     for (int i = 0; i < e->nents; i++) if (e->ents[i].kind == ENT_BLOCK) { shape = i; break; }
     vec2 p = e->space.bodies[e->ents[shape].body0].p;
-    double s2c = np_norm2(p.x - 0.0, p.y - 1.0);
-    double r2s = np_norm2(r.x - p.x, r.y - p.y);
+    return o_shaped_move_to_corner(r.x, r.y, p.x, p.y);
+}
+
+/* move_to_corner.py:86-100 debug_shaped_reward on (robot, block) positions */
+double o_shaped_move_to_corner(double rx, double ry, double sx, double sy) {
+    double s2c = np_norm2(sx - 0.0, sy - 1.0);
+    double r2s = np_norm2(rx - sx, ry - sy);
     double shaping = -s2c / 5 - (r2s > 0.2 ? r2s : 0.2) / 20;
-    return shaping + oscene_score(e);
+    return shaping + o_score_move_to_corner(rx, ry);
 }
 
 double oscene_score(OEnv *e) {

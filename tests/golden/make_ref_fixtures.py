@@ -28,8 +28,27 @@ written out: the JSON files hold inputs and the reference's outputs only.
   * ref_make_line.json -- benchmarks/make_line.py:31-72 (longest_line) on random
                         point sets and on near-collinear sets that sit at the
                         scorer's inlier / separation thresholds.
+  * ref_wrappers.json -- benchmarks/__init__.py:31-307: the preprocessor entry
+                        points of every LoRes name (lores_ea_entry_point /
+                        lores_stack_entry_point with FlattenFrameStack /
+                        EagerDictFrameStack, ResizeDictObservation, ChannelsFirst),
+                        run on synthetic 384^2 frame sequences with resets; gym's
+                        Wrapper / Box / Dict, SB3's is_image_space and cv2.resize
+                        are stand-ins (cv2 INTER_AREA 4x = the oracle's
+                        o_downsample, pinned separately).  Stored: observation
+                        keys, shapes, dtypes and a sha256 per value and event.
+  * ref_scorers.json  -- cluster.py:166-216 (BaseClusterEnv.score_on_end_of_traj)
+                        on random, clustered and near-threshold block layouts;
+                        move_to_corner.py:67-100 (score_on_end_of_traj and
+                        debug_shaped_reward) on random robot / block positions.
+  * ref_actions.json  -- entities.py:148-190 (RobotAction, ACTION_NUMS_FLAGS_NAMES)
+                        and Robot.set_action (:435-453) for every action id.
 """
 import ast
+import collections
+import enum
+import functools
+import hashlib
 import importlib.util
 import itertools
 import json
@@ -46,11 +65,20 @@ REF = "/root/reference/magical"
 sys.dont_write_bytecode = True
 
 
+def _node_name(n):
+    if isinstance(n, (ast.FunctionDef, ast.ClassDef)):
+        return n.name
+    if isinstance(n, ast.Assign) and len(n.targets) == 1 and isinstance(n.targets[0], ast.Name):
+        return n.targets[0].id
+    return None
+
+
 def _extract(path, names, namespace):
-    """Execute the top-level definitions `names` of the reference file `path` in `namespace`."""
+    """Execute the top-level definitions / assignments `names` of the reference file `path` in `namespace`
+    (in file order)."""
     tree = ast.parse(open(path).read(), filename=path)
-    nodes = [n for n in tree.body if isinstance(n, (ast.FunctionDef, ast.ClassDef)) and n.name in names]
-    missing = set(names) - {n.name for n in nodes}
+    nodes = [n for n in tree.body if _node_name(n) in names]
+    missing = set(names) - {_node_name(n) for n in nodes}
     assert not missing, missing
     mod = ast.Module(body=nodes, type_ignores=[])
     exec(compile(mod, path, "exec"), namespace)
@@ -242,9 +270,202 @@ def ref_make_line():
     return {"inlier_dist": inlier, "max_sep": sep, "cases": out}
 
 
+# ---- preprocessor wrappers (benchmarks/__init__.py) -----------------------------------------------
+class _Box:
+    """stand-in for gym.spaces.Box (bounds as arrays, like gym 0.17)"""
+
+    def __init__(self, low, high, shape=None, dtype=np.float32):
+        dtype = np.dtype(dtype)
+        if shape is not None:
+            low, high = np.full(shape, low, dtype=dtype), np.full(shape, high, dtype=dtype)
+        self.low, self.high = np.asarray(low, dtype=dtype), np.asarray(high, dtype=dtype)
+        self.shape, self.dtype = self.low.shape, dtype
+
+
+class _Dict:
+    def __init__(self, spaces):
+        self.spaces = collections.OrderedDict(spaces)
+
+    def __getitem__(self, k):
+        return self.spaces[k]
+
+    def __setitem__(self, k, v):
+        self.spaces[k] = v
+
+
+class _Wrapper:
+    def __init__(self, env):
+        self.env = env
+        self.observation_space = env.observation_space
+
+    def step(self, action):
+        return self.env.step(action)
+
+    def reset(self, **kwargs):
+        return self.env.reset(**kwargs)
+
+
+class _ObservationWrapper(_Wrapper):
+    def step(self, action):
+        o, r, d, i = self.env.step(action)
+        return self.observation(o), r, d, i
+
+    def reset(self, **kwargs):
+        return self.observation(self.env.reset(**kwargs))
+
+
+def _is_image_space(box):
+    """stable_baselines3.common.preprocessing.is_image_space (channels-last uint8 Box in [0, 255])"""
+    return isinstance(box, _Box) and len(box.shape) == 3 and box.dtype == np.uint8 and \
+        np.all(box.low == 0) and np.all(box.high == 255)
+
+
+def _cv2_resize(img, size, interpolation=None):
+    """cv2.resize(INTER_AREA) 384^2 -> 96^2, per channel: the oracle's o_downsample on each 3 channels"""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "oracle"))
+    import pyoracle as po
+    assert img.shape[:2] == (384, 384) and tuple(size) == (96, 96) and img.shape[2] % 3 == 0
+    return np.concatenate([po.downsample(np.ascontiguousarray(img[..., c:c + 3])) for c in range(0, img.shape[2], 3)],
+                          axis=-1)
+
+
+class SyntheticFrames:
+    """Base env emitting random 384^2 allo / ego frames: the j-th observation of a case is
+    RandomState(1000 * case + j).randint(0, 256, (2, 384, 384, 3), dtype=uint8)."""
+
+    def __init__(self, case):
+        self.case, self.j = case, 0
+        img = _Box(0, 255, (384, 384, 3), np.uint8)
+        self.observation_space = _Dict([("allo", img), ("ego", _Box(0, 255, (384, 384, 3), np.uint8))])
+
+    def _obs(self):
+        f = np.random.RandomState(1000 * self.case + self.j).randint(0, 256, (2, 384, 384, 3), dtype=np.uint8)
+        self.j += 1
+        return collections.OrderedDict([("allo", f[0]), ("ego", f[1])])
+
+    def reset(self):
+        return self._obs()
+
+    def step(self, action):
+        return self._obs(), 0.0, False, {}
+
+
+WRAPPER_EVENTS = ["reset", "step", "step", "step", "step", "step", "reset", "step", "step"]
+
+
+def _digest(a):
+    a = np.ascontiguousarray(a)
+    return hashlib.sha256(a.tobytes()).hexdigest()
+
+
+def ref_wrappers():
+    gym = types.SimpleNamespace(Wrapper=_Wrapper, ObservationWrapper=_ObservationWrapper,
+                                spaces=types.SimpleNamespace(Box=_Box, Dict=_Dict))
+    ns = {"__name__": "ref_wrappers", "np": np, "collections": collections, "functools": functools,
+          "gym": gym, "Box": _Box, "Dict": _Dict, "Discrete": None, "Optional": typing.Optional,
+          "is_image_space": _is_image_space, "cv2": types.SimpleNamespace(resize=_cv2_resize, INTER_AREA=3),
+          "ResizeObservation": None, "cls_lookup": None}
+    _extract(os.path.join(REF, "benchmarks", "__init__.py"),
+             ["_gym_tree_map", "EagerDictFrameStack", "FlattenFrameStack", "ResizeDictObservation", "ChannelsFirst",
+              "get_cls", "lores_stack_entry_point", "lores_ea_entry_point", "DEFAULT_PREPROC_ENTRY_POINT_WRAPPERS"], ns)
+    out = {"events": WRAPPER_EVENTS, "cases": []}
+    for case, (pp, make) in enumerate(ns["DEFAULT_PREPROC_ENTRY_POINT_WRAPPERS"].items()):
+        env = make(lambda c=case: SyntheticFrames(c))()
+        space = [[k, list(b.shape), str(b.dtype)] for k, b in env.observation_space.spaces.items()]
+        obs_log = []
+        for ev in WRAPPER_EVENTS:
+            o = env.reset() if ev == "reset" else env.step(0)[0]
+            obs_log.append([[k, list(np.shape(v)), str(np.asarray(v).dtype), _digest(v)] for k, v in o.items()])
+        out["cases"].append({"preproc": pp, "case": case, "space": space, "obs": obs_log})
+    return out
+
+
+# ---- scorers and the action table --------------------------------------------------------------------
+def _pos(x, y):
+    return types.SimpleNamespace(shape_body=types.SimpleNamespace(position=types.SimpleNamespace(x=float(x), y=float(y))))
+
+
+def ref_scorers():
+    class _Base:
+        pass
+
+    ns = {"__name__": "ref_cluster", "np": np, "abc": __import__("abc"), "enum": enum, "BaseEnv": _Base, "EzPickle": object, "ez_init": lambda **k: (lambda f: f)}
+    _extract(os.path.join(REF, "benchmarks", "cluster.py"), ["BaseClusterEnv"], ns)
+    C = ns["BaseClusterEnv"]
+    rs = np.random.RandomState(31)
+    values = ["blue", "green", "red", "yellow"]
+    cases = []
+
+    def run(vals, xy):
+        env = object.__new__(C)
+        by = {}
+        for v, (x, y) in zip(vals, xy):
+            by.setdefault(values[v], []).append(_pos(x, y))
+        env._BaseClusterEnv__characteristic_values = np.unique([values[v] for v in vals])
+        env._BaseClusterEnv__blocks_by_characteristic = by
+        return float(env.score_on_end_of_traj())
+
+    for k in range(600):
+        n = int(rs.randint(7, 11))
+        vals = list(range(4)) + list(rs.randint(0, 4, n - 4))
+        rs.shuffle(vals)
+        kind = k % 3
+        if kind == 0:     # random layout
+            xy = rs.uniform(-1, 1, (n, 2))
+        else:             # clustered around per-value centres, spread scanned across the margin threshold
+            centres = rs.uniform(-0.7, 0.7, (4, 2))
+            spread = rs.choice([0.02, 0.05, 0.08, 0.1, 0.12, 0.15, 0.2]) if kind == 1 else rs.uniform(0.03, 0.2)
+            xy = centres[vals] + rs.normal(0, spread, (n, 2))
+        cases.append({"vals": [int(v) for v in vals], "xy": xy.ravel().tolist(), "score": run(vals, xy)})
+    mtc_ns = {"__name__": "ref_mtc", "np": np, "math": math, "BaseEnv": _Base, "EzPickle": object,
+              "ez_init": lambda **k: (lambda f: f), "warnings": None, "geom": None, "en": None}
+    _extract(os.path.join(REF, "benchmarks", "move_to_corner.py"), ["MoveToCornerEnv"], mtc_ns)
+    M = mtc_ns["MoveToCornerEnv"]
+    mtc = []
+    for k in range(600):
+        r = rs.uniform(-1.2, 1.2, 2) if k % 4 else np.array([-1.0, 1.0]) + rs.uniform(-0.8, 0.8, 2)
+        sh = rs.uniform(-1.2, 1.2, 2) if k % 5 else r + rs.uniform(-0.25, 0.25, 2)
+        env = object.__new__(M)
+        env.robot = types.SimpleNamespace(robot_body=types.SimpleNamespace(position=(float(r[0]), float(r[1]))))
+        env._robot = env.robot
+        env._MoveToCornerEnv__shape_ref = types.SimpleNamespace(
+            shape_body=types.SimpleNamespace(position=(float(sh[0]), float(sh[1]))))
+        mtc.append({"robot": r.tolist(), "shape": sh.tolist(), "score": float(env.score_on_end_of_traj()),
+                    "shaped": float(env.debug_shaped_reward())})
+    return {"cluster_values": values, "cluster": cases, "move_to_corner": mtc}
+
+
+def ref_actions():
+    ns = {"__name__": "ref_entities", "enum": enum}
+    _extract(os.path.join(REF, "entities.py"),
+             ["RobotAction", "ACTION_NUMS_FLAGS_NAMES", "ACTION_ID_TO_FLAGS", "FLAGS_TO_ACTION_ID"], ns)
+    tree = ast.parse(open(os.path.join(REF, "entities.py")).read())
+    robot = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "Robot")
+    set_action = next(n for n in robot.body if isinstance(n, ast.FunctionDef) and n.name == "set_action")
+    exec(compile(ast.Module(body=[set_action], type_ignores=[]), "entities.py", "exec"), ns)
+    rows = []
+    for act_id, flags, name in ns["ACTION_NUMS_FLAGS_NAMES"]:
+        bot = types.SimpleNamespace(radius=0.2, finger_rot_limit_outer=math.pi / 8, finger_rot_limit_inner=0,
+                                    target_finger_angle=123.0)
+        action_flag = ns["RobotAction"].NONE
+        for f in flags:
+            action_flag |= f
+        ns["set_action"](bot, action_flag)
+        rows.append({"id": act_id, "flags": [int(f) for f in flags], "name": name, "bits": int(action_flag),
+                     "target_speed": bot.target_speed, "rel_turn_angle": bot.rel_turn_angle,
+                     "target_finger_angle": float(bot.target_finger_angle),
+                     "flags_to_action": ns["FLAGS_TO_ACTION_ID"][tuple(flags)]})
+    return {"actions": rows, "flag_values": {m.name: int(m.value) for m in ns["RobotAction"]}}
+
+
 def main():
-    for fn, data in (("ref_render.json", ref_render()), ("ref_make_line.json", ref_make_line()),
-                     ("ref_outline.json", ref_outline())):
+    only = set(sys.argv[1:])
+    for fn, make in (("ref_render.json", ref_render), ("ref_make_line.json", ref_make_line),
+                     ("ref_outline.json", ref_outline), ("ref_wrappers.json", ref_wrappers),
+                     ("ref_scorers.json", ref_scorers), ("ref_actions.json", ref_actions)):
+        if only and fn not in only:
+            continue
+        data = make()
         with open(os.path.join(HERE, fn), "w") as f:
             json.dump(data, f, indent=None, separators=(",", ":"))
             f.write("\n")

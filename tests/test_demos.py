@@ -63,25 +63,7 @@ def test_load_demos_rewrites_imitation_trajectory_class(tmp_path):
 
 
 def _oracle_stack(lo, starts, preproc):
-    """Per-frame LoRes dicts from per-frame downsampled (allo, ego), by the reference wrappers' rules."""
-    out = []
-    for f in range(len(lo)):
-        back = lambda k: max(f - k, starts[f])  # noqa: E731
-        if preproc == "LoResStack":
-            out.append(collections.OrderedDict(
-                (k, np.concatenate([lo[back(j)][v] for j in (3, 2, 1, 0)], axis=-1)) for v, k in enumerate(("allo", "ego"))))
-            continue
-        if preproc == "LoRes3EA":
-            frames = [lo[f][0]] + [lo[back(j)][1] for j in (2, 1, 0)]
-        elif preproc == "LoRes4A":
-            frames = [lo[back(j)][0] for j in (3, 2, 1, 0)]
-        else:
-            frames = [lo[back(j)][1] for j in (3, 2, 1, 0)]
-        d = collections.OrderedDict([("allo", lo[f][0]), ("ego", lo[f][1]), ("past_obs", np.concatenate(frames, -1))])
-        if registry.PREPROCESSORS[preproc].get("channels_first", False):
-            d = collections.OrderedDict((k, np.moveaxis(v, -1, 0)) for k, v in d.items())
-        out.append(d)
-    return out
+    return po.stack_lores(lo, starts, preproc, registry.PREPROCESSORS[preproc].get("channels_first", False))
 
 
 def _rollout_frames(name, seed, steps):
@@ -149,3 +131,34 @@ def test_replay_rejects_bad_arguments():
         demos.replay_lores(torch.zeros((1, 2, 384, 384, 3), dtype=torch.uint8, device="cuda"), [0], "HiRes")
     with pytest.raises(ValueError):
         demos.replay_lores(torch.zeros((1, 2, 96, 96, 3), dtype=torch.uint8, device="cuda"), [0], "LoRes4E")
+
+
+@pytest.mark.gpu
+def test_replay_matches_reference_wrapper_fixtures():
+    """mg_replay_lores (through preprocess_demos_with_wrapper) on the synthetic frame sequences of
+    tests/golden/ref_wrappers.json -- the REFERENCE's own entry points executed in the build container --
+    gives the reference's observations bit for bit (sha256), for every LoRes preprocessor, with the
+    sequence's mid-point reset as a second trajectory."""
+    import hashlib
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_wrappers.json")))
+    ev = g["events"]
+    cut = ev.index("reset", 1)
+    for case in g["cases"]:
+        frames = [np.random.RandomState(1000 * case["case"] + j).randint(0, 256, (2, 384, 384, 3), dtype=np.uint8)
+                  for j in range(len(ev))]
+        trajs = []
+        for lo, hi in ((0, cut), (cut, len(ev))):
+            obs = [{"allo": f[0], "ego": f[1]} for f in frames[lo:hi]]
+            k = hi - lo - 1
+            trajs.append(demos.MAGICALTrajectory(acts=np.zeros(k, np.int64), obs=obs, rews=np.zeros(k, np.float32),
+                                                 infos=[{}] * k))
+        out = demos.preprocess_demos_with_wrapper(trajs, "MoveToCorner-Demo-v0", case["preproc"])
+        got = out[0].obs + out[1].obs
+        for j, ref in enumerate(case["obs"]):
+            assert [k for k, *_ in ref] == list(got[j]), (case["preproc"], j)
+            for k, shape, dtype, h in ref:
+                v = np.ascontiguousarray(got[j][k])
+                assert list(v.shape) == shape and str(v.dtype) == dtype, (case["preproc"], j, k)
+                assert hashlib.sha256(v.tobytes()).hexdigest() == h, (case["preproc"], j, k)

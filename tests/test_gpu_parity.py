@@ -624,39 +624,88 @@ def test_layout_retry_parity(name, tries, monkeypatch):
     vec.close()
 
 
+GATHER_GPU_CASES = [("MoveToRegion-Demo-LoRes4E-v0", "frames", 40), ("MoveToRegion-Demo-LoRes4E-v0", "stacked", 40),
+                    ("MoveToRegion-Demo-LoResCHW4E-v0", "frames", 40), ("ClusterColour-Demo-LoResStack-v0", "frames", 12),
+                    ("ClusterColour-Demo-LoResStack-v0", "stacked", 12), ("MoveToCorner-Demo-LoRes3EA-v0", "frames", 15),
+                    ("MoveToCorner-Demo-LoRes4A-v0", "frames", 15), ("PickAndPlace-Demo-LoRes4E-v0", "frames", 15)]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["MoveToRegion-Demo-LoRes4E-v0", "MoveToRegion-Demo-LoResCHW4E-v0"])
-def test_packed_gather_pipeline_single_rank(tmp_path, name):
+@pytest.mark.parametrize("name,mode,L", GATHER_GPU_CASES)
+def test_packed_gather_pipeline_single_rank(tmp_path, name, mode, L):
     """The multi-GPU exchange path on one GPU (a 1-rank RCCL group): the simulator writes each step's
-    outputs straight into views of a packed buffer (bind_outputs), one all_gather_into_tensor per step
-    on a side stream, two buffers alternating; every step's gathered [1, n, ...] views equal a plain
-    VecMagicalEnv run bit for bit (obs, reward, done, eval_score), incl. the CHW views."""
+    outputs straight into views of a packed buffer (bind_outputs; gather_mode 'frames': the current frames
+    only), one all_gather_into_tensor per step on a side stream, then (frames) the receiver-side restack
+    kernel mg_restack rebuilds the frame stacks; two buffer sets alternate.  Every step's gathered
+    [1, n, ...] results equal a plain VecMagicalEnv run bit for bit (obs incl. the rebuilt stacks and the
+    CHW views, reward, done, eval_score, PickAndPlace's target), over 45 steps that cross auto-resets
+    (episode length L)."""
     import torch.distributed as dist
     from magical_amd import dist as mdist
     n, steps = 70, 45
     dist.init_process_group("nccl", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     try:
-        shard = mdist.ShardedVecEnv(name, n, rank=0, device="cuda:0", gather=True)
-        ref = magical_amd.make_vec(name, n, seeds=mdist.shard_seeds(n, 0))
+        shard = mdist.ShardedVecEnv(name, n, rank=0, device="cuda:0", gather=True, gather_mode=mode,
+                                    max_episode_steps=L)
+        ref = magical_amd.make_vec(name, n, seeds=mdist.shard_seeds(n, 0), max_episode_steps=L)
         acts = np.random.RandomState(4).randint(0, 18, (steps, n))
         got = shard.reset()
         want = ref.reset()
+        assert list(got) == list(want)
         for k in want:
             assert torch.equal(got[k][0], want[k]), f"reset {k}"
-        handles = []
+        handles, resets = [], 0
         for t in range(steps):
             a = torch.as_tensor(acts[t], dtype=torch.uint8)
             handles.append(shard.step_async(a))
             obs, rew, done, info = ref.step(a)
-            if t >= 1:   # the previous step's gather, read after this step was launched
+            resets += int(done.sum().item())
+            if t >= 1:   # the previous step's exchange, read after this step was launched
                 g_obs, g_rew, g_done, g_info = handles[t - 1].results()
+                assert list(g_obs) == list(prev[0])
                 for k in prev[0]:
                     assert torch.equal(g_obs[k][0], prev[0][k]), f"step {t - 1} {k}"
                 assert torch.equal(g_rew[0], prev[1]) and torch.equal(g_done[0], prev[2])
                 assert torch.equal(g_info["eval_score"][0], prev[3])
-            prev = ({k: v.clone() for k, v in obs.items()}, rew.clone(), done.clone(), info["eval_score"].clone())
+                if "target" in g_info:
+                    assert torch.equal(g_info["target"][0], prev[4]), f"step {t - 1} target"
+            prev = ({k: v.clone() for k, v in obs.items()}, rew.clone(), done.clone(), info["eval_score"].clone(),
+                    ref.target.clone() if ref.target is not None else None)
+        assert resets >= n * (steps // L - 1)
         shard.close()
         ref.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("preproc", ["LoRes4E", "LoResStack", "LoRes3EA", "LoRes4A"])
+def test_restack_kernel_matches_oracle_rule(preproc):
+    """mg_restack on synthetic gathered batches (world 3, 37 envs per rank: a ragged last workgroup) with
+    random frames and random done flags over 9 steps, an all-fresh reset first and again in the middle:
+    the stacks equal the oracle's restatement of the reference's frame-stack rule bit for bit."""
+    from magical_amd import dist as mdist, registry
+    name = {"LoRes4E": "MoveToRegion-Demo-LoRes4E-v0", "LoResStack": "ClusterColour-Demo-LoResStack-v0",
+            "LoRes3EA": "MoveToRegion-Demo-LoRes3EA-v0", "LoRes4A": "MoveToRegion-Demo-LoRes4A-v0"}[preproc]
+    spec = registry.lookup(name)
+    W, n = 3, 37
+    lay = mdist.PackedLayout.for_spec(spec, n, frames_only=True)
+    nat = mdist.NativeRestacker(lay, W, torch.device("cuda", 0))
+    orc = po.OracleRestacker(lay, preproc)
+    rs = np.random.RandomState(11)
+    keys = mdist.stacked_keys(preproc)
+    for t in range(9):
+        recv = torch.from_numpy(rs.randint(0, 256, W * lay.nbytes).astype(np.uint8))
+        v = lay.unpack(recv)
+        v["done"].copy_(torch.from_numpy(rs.rand(W, n) < 0.2))
+        fresh = t in (0, 5)
+        out_c = {k: torch.zeros((W * n, 96, 96, 12), dtype=torch.uint8) for k in keys}
+        out_g = {k: torch.zeros((W * n, 96, 96, 12), dtype=torch.uint8, device="cuda") for k in keys}
+        orc(recv, out_c, t, fresh)
+        nat(recv.cuda(), out_g, t, fresh)
+        torch.cuda.synchronize()
+        for k in keys:
+            assert torch.equal(out_g[k].cpu(), out_c[k]), (t, k)
+
+

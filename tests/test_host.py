@@ -185,7 +185,7 @@ def test_two_rank_gloo_sharded_rollout_equals_single_process(tmp_path):
     assert np.array_equal(full, ref)
 
 
-PACKED_WORKER = r'''
+PACKED_WORKER = r"""
 import os, sys
 sys.path[:0] = [{root!r} + "/magical-1_amd", {root!r} + "/oracle"]
 import numpy as np, torch, torch.distributed as dist
@@ -193,63 +193,127 @@ import pyoracle as po
 from magical_amd import dist as mdist, registry, envs as mg_envs
 rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 dist.init_process_group("gloo", init_method="env://")
-name = {name!r}
+name, mode, L = {name!r}, {mode!r}, {L}
 spec = registry.lookup(name)
-n, steps = 2, 7
+n, steps = 2, {steps}
+CHW = registry.PREPROCESSORS[spec.preproc].get("channels_first", False)
 
 class OracleVec:
-    """CPU stand-in for VecMagicalEnv's output binding: the oracle writes each step into the bound views"""
+    # CPU stand-in for VecMagicalEnv's output binding: the oracle writes each step into the bound views
+    # (frames_only: the current frame of each view only, as the simulator's frames-only mode does)
     device = torch.device("cpu")
     def __init__(self, seeds):
-        self.envs = [po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, spec.max_episode_steps, seed=s) for s in seeds]
-    def bind_outputs(self, views):
-        self.v = views
+        self.envs = [po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, L, seed=s) for s in seeds]
+        self.target = torch.zeros((len(seeds), 4), dtype=torch.float64) if spec.task == "PickAndPlace" else None
+    def bind_outputs(self, views, frames_only=False):
+        self.v, self.fo = views, frames_only
     def _write(self, i, flat, r=0.0, d=False, sc=0.0):
         off = 0
         for k, s in mg_envs._obs_shapes(spec).items():
             m = int(np.prod(s))
-            self.v[k][i].copy_(torch.from_numpy(flat[off:off + m].reshape(self.v[k][i].shape)))
+            a = flat[off:off + m].reshape(s)
             off += m
+            if CHW:   # the oracle writes channels-first bytes; the bound buffers are HWC
+                a = a.transpose(1, 2, 0)
+            if self.fo:
+                if k == "past_obs":
+                    continue
+                a = a[..., 9:12] if a.shape[-1] == 12 else a   # LoResStack: the newest frame of the stack
+            self.v[k][i].copy_(torch.from_numpy(np.ascontiguousarray(a)).reshape(self.v[k][i].shape))
         self.v["reward"][i] = r; self.v["done"][i] = d; self.v["eval_score"][i] = sc
+    def _reset_one(self, i):
+        o = self.envs[i].reset()
+        if self.target is not None:
+            self.target[i] = torch.from_numpy(self.envs[i].target())
+        return o
     def reset(self):
-        for i, e in enumerate(self.envs):
-            self._write(i, e.reset())
+        for i in range(len(self.envs)):
+            self._write(i, self._reset_one(i))
     def step(self, actions):
         for i, e in enumerate(self.envs):
             o, r, d, sc = e.step(int(actions[i]))
             if d:
-                o = e.reset()
+                o = self._reset_one(i)
             self._write(i, o, r, d, sc)
     def close(self):
         pass
 
 vec = OracleVec(mdist.shard_seeds(n, rank))
-env = mdist.ShardedVecEnv(name, n, rank=rank, gather=True, vec=vec, device="cpu")
+lay = mdist.PackedLayout.for_spec(spec, n, frames_only=mode == "frames")
+env = mdist.ShardedVecEnv(name, n, rank=rank, gather=True, vec=vec, device="cpu", gather_mode=mode,
+                          restacker=po.OracleRestacker(lay, spec.preproc) if mode == "frames" else None)
 acts = np.random.RandomState(5).randint(0, 18, (steps, world * n))
 lo, hi = mdist.shard_range(n, rank)
-obs = env.reset()
-handles = []
+rec = {{}}
+def keep(t, obs, rew=None, done=None, info=None):
+    for k, v in obs.items():
+        rec.setdefault(k, []).append(v.clone().numpy())
+    if rew is not None:
+        rec.setdefault("reward", []).append(rew.clone().numpy()); rec.setdefault("done", []).append(done.clone().numpy())
+        rec.setdefault("score", []).append(info["eval_score"].clone().numpy())
+        if "target" in info:
+            rec.setdefault("target", []).append(info["target"].clone().numpy())
+keep(-1, env.reset())
+prev = None
 for t in range(steps):
-    handles.append(env.step_async(torch.as_tensor(acts[t, lo:hi])))
-obs, rew, done, info = handles[-1].results()
+    h = env.step_async(torch.as_tensor(acts[t, lo:hi]))
+    if prev is not None:      # the previous step's exchange, read after this step was launched
+        keep(t - 1, *prev.results())
+    prev = h
+keep(steps - 1, *prev.results())
 if rank == 0:
-    np.savez({out!r}, **{{k: v.numpy() for k, v in obs.items()}}, reward=rew.numpy(), done=done.numpy(),
-             score=info["eval_score"].numpy(), nbytes=env.layout.nbytes)
+    np.savez({out!r}, nbytes=env.layout.nbytes, stacked_nbytes=env.stacked_nbytes,
+             **{{k: np.stack(v) for k, v in rec.items()}})
 env.close()
 dist.destroy_process_group()
-'''
+"""
+
+def test_bench_launches_ranks_itself():
+    """bench.py --gpus 2 without WORLD_SIZE re-runs itself under torch.distributed.run with 2 ranks
+    (before any GPU call); --dry-run swaps the GPU work for a gloo all-reduce, so rank 0 sees 2 ranks and
+    the N > 1 gather default is on."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["ranks_seen"] == 2 and line["n_gpus"] == 2 and line["gather"] is True
 
 
-@pytest.mark.parametrize("name", ["MoveToRegion-Demo-LoRes4E-v0", "ClusterColour-Demo-LoResStack-v0"])
-def test_two_rank_gloo_packed_gather_pipeline(tmp_path, name):
-    """ShardedVecEnv(gather=True) with world_size 2 on CPU tensors: each rank's step outputs are
-    written into views of one packed buffer, one all_gather_into_tensor per step, two buffers
-    alternating (step_async handles of 7 steps kept, the last one read).  The unpacked [W, n, ...]
-    views equal one process running all W * n envs: observations, reward, done, eval_score,
-    across an episode boundary (MoveToRegion: done at 40 is not reached; LoResStack keys)."""
+def test_bench_byte_models():
+    """Per-kernel algorithmic bytes: render = observations + frame ring (frames-only mode: 2 frames), restack =
+    per stacked view 1 + 3 frames read, 1 + 4 frames written."""
+    sys.path.insert(0, ROOT)
+    import bench
+    fr = 96 * 96 * 3
+    assert bench.render_bytes("LoRes4E") == 165888 + 4 * fr
+    assert bench.render_bytes("LoResStack") == 221184 + 8 * fr
+    assert bench.render_bytes("LoRes4E", frames_only=True) == 2 * fr
+    assert bench.restack_bytes("LoResStack") == 2 * 9 * fr
+
+
+GATHER_CASES = [("MoveToRegion-Demo-LoRes4E-v0", "frames"), ("MoveToRegion-Demo-LoRes4E-v0", "stacked"),
+                ("ClusterColour-Demo-LoResStack-v0", "frames"), ("ClusterColour-Demo-LoResStack-v0", "stacked"),
+                ("MoveToCorner-Demo-LoRes3EA-v0", "frames"), ("MoveToCorner-Demo-LoRes4A-v0", "frames"),
+                ("MoveToRegion-Demo-LoResCHW4E-v0", "frames"), ("PickAndPlace-Demo-LoRes4E-v0", "frames")]
+
+
+@pytest.mark.parametrize("name,mode", GATHER_CASES)
+def test_two_rank_gloo_packed_gather_pipeline(tmp_path, name, mode):
+    """ShardedVecEnv(gather=True) with world_size 2 on CPU tensors, episodes of 5 steps (max_episode_steps)
+    so the 12 steps cross two auto-resets of every env: each rank's step outputs are written into views of
+    one packed buffer, one all_gather_into_tensor per step, two buffer sets alternating (each step's
+    handle read after the next step was launched).  gather_mode 'frames' gathers only the current frames
+    and rebuilds the stacks on the receiver (here with the oracle's restacker; the GPU kernel mg_restack
+    is checked against the simulator in tests/test_gpu_parity.py).  Every step's [W, n, ...] results --
+    observations (incl. rebuilt stacks across the resets), reward, done, eval_score, PickAndPlace's
+    target -- equal one process running all W * n envs.  'frames' moves 3x (LoRes4E) / 4x (LoResStack)
+    fewer bytes per rank-step than 'stacked'."""
     out = str(tmp_path / "full.npz")
     script = tmp_path / "worker.py"
-    script.write_text(PACKED_WORKER.format(root=ROOT, out=out, name=name))
+    L, steps = 5, 12
+    script.write_text(PACKED_WORKER.format(root=ROOT, out=out, name=name, mode=mode, L=L, steps=steps))
     port = _free_port()
     procs = []
     for r in range(2):
@@ -262,24 +326,43 @@ def test_two_rank_gloo_packed_gather_pipeline(tmp_path, name):
     import pyoracle as po
     from magical_amd import envs as mg_envs
     spec = registry.lookup(name)
-    steps, W, n = 7, 2, 2
+    W, n = 2, 2
     acts = np.random.RandomState(5).randint(0, 18, (steps, W * n))
-    envs = [po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, spec.max_episode_steps, seed=1000 + i)
-            for i in range(W * n)]
-    for e in envs:
-        e.reset()
-    for t in range(steps):
-        res = [e.step(int(a)) for e, a in zip(envs, acts[t])]
+    envs = [po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, L, seed=1000 + i) for i in range(W * n)]
     shapes = mg_envs._obs_shapes(spec)
-    for i, (o, r, d, sc) in enumerate(res):
+    chw = registry.PREPROCESSORS[spec.preproc].get("channels_first", False)
+
+    def check(t, i, o, res=None, target=None):
         off = 0
         for k, s in shapes.items():
             m = int(np.prod(s))
-            assert np.array_equal(got[k][i // n, i % n], o[off:off + m].reshape(s)), (k, i)
+            assert np.array_equal(got[k][t + 1, i // n, i % n], o[off:off + m].reshape(s)), (t, k, i)
             off += m
-        assert got["reward"][i // n, i % n] == np.float32(r) and bool(got["done"][i // n, i % n]) == d
-        assert got["score"][i // n, i % n] == sc
+        if res is not None:
+            r, d, sc = res
+            assert got["reward"][t, i // n, i % n] == np.float32(r) and bool(got["done"][t, i // n, i % n]) == d
+            assert got["score"][t, i // n, i % n] == sc
+        if target is not None:
+            assert np.array_equal(got["target"][t, i // n, i % n], target), (t, i)
+            assert np.array_equal(got["target_position"][t + 1, i // n, i % n], target[2:4].astype(np.float32))
+
+    for i, e in enumerate(envs):
+        check(-1, i, e.reset())
+    crossed = 0
+    for t in range(steps):
+        for i, e in enumerate(envs):
+            o, r, d, sc = e.step(int(acts[t, i]))
+            if d:
+                o = e.reset()
+                crossed += 1
+            check(t, i, o, (r, d, sc), e.target() if spec.task == "PickAndPlace" else None)
+    assert crossed == 2 * W * n
+    if chw:
+        assert got["past_obs"].shape[-3:] == (12, 96, 96)
     assert int(got["nbytes"]) % 256 == 0
+    if mode == "frames":
+        ratio = int(got["stacked_nbytes"]) / int(got["nbytes"])
+        assert ratio > (3.9 if spec.preproc == "LoResStack" else 2.9), ratio
 
 
 # --------------------------------------------------------------------------- evaluation protocol
