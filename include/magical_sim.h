@@ -82,7 +82,10 @@ int mg_get_bodies(mg_sim *sim, double *out_dev, int32_t *counts_dev, void *strea
 /* set body `body` of env `env` to (x, y, angle) like pymunk's Body.position / Body.angle setters
  * (geom.py:362-384 pm_shift_bodies applies them); for parity tests that place blocks before a step */
 int mg_set_body_pose(mg_sim *sim, int env, int body, double x, double y, double angle, void *stream);
-/* per-env error flags (table overflow, placement failure, raster assumption): device i32[N] */
+/* per-env error flags, device i32[N]: 1 arbiter table full, 2 PlacementError in the env's latest reset
+ * (geom.py:335-336; cleared by the next reset, which draws a new layout), 64 PlacementError in any reset so
+ * far (sticky), 4 / 8 allo / ego raster assumption or capacity, 16 / 32 scene outside the step kernel's
+ * compiled caps / constraint list */
 int mg_get_errors(mg_sim *sim, int32_t *out_dev, void *stream);
 /* re-seed env RNGs (env.seed): host u32[num_envs] */
 int mg_seed(mg_sim *sim, const uint32_t *seeds_host);

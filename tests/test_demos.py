@@ -155,7 +155,7 @@ def test_replay_matches_reference_wrapper_fixtures():
             trajs.append(demos.MAGICALTrajectory(acts=np.zeros(k, np.int64), obs=obs, rews=np.zeros(k, np.float32),
                                                  infos=[{}] * k))
         out = demos.preprocess_demos_with_wrapper(trajs, "MoveToCorner-Demo-v0", case["preproc"])
-        got = out[0].obs + out[1].obs
+        got = list(out[0].obs) + list(out[1].obs)
         for j, ref in enumerate(case["obs"]):
             assert [k for k, *_ in ref] == list(got[j]), (case["preproc"], j)
             for k, shape, dtype, h in ref:
