@@ -116,36 +116,17 @@ __global__ __launch_bounds__(256) void replay_assemble_kernel(const uint8_t *__r
 }
 
 // Receiver-side frame stacks of the compact multi-GPU gather (mg_restack, magical_amd.dist): one thread per
-// 16 pixels (48 B of a frame: three 16-byte loads) of one env and one output stack (blockIdx.y: LoResStack
-// 0 allo / 1 ego; else 0 = past_obs).  The ring view of the stack keeps the env's last 4 frames (slot
-// t % 4 = this step); a fresh env (reset, or done = auto-reset) fills every slot with its current frame,
-// as the deques of benchmarks/__init__.py:75-82,139-147 are filled at reset.  Byte work per env and stack:
-// 27 648 B read (+ 82 944 B of ring unless fresh), 27 648 B ring write and 110 592 B stacked output --
-// HBM bound; the ring and the stacks are written with non-temporal stores (streamed, read again only a
-// step or more later).
-constexpr int RS_PIX = 16;                              // pixels per thread
-constexpr int RS_W = RS_PIX * 3 / 4;                    // dwords of one frame per thread (12)
-
-__device__ __forceinline__ void ld12(const uint8_t *p, uint32_t (&f)[RS_W]) {
-    const uint4 *q = (const uint4 *)p;
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-        const uint4 v = q[i];
-        f[4 * i] = v.x; f[4 * i + 1] = v.y; f[4 * i + 2] = v.z; f[4 * i + 3] = v.w;
-    }
-}
-__device__ __forceinline__ void st12_nt(uint8_t *p, const uint32_t (&f)[RS_W]) {
-    uint32_t *q = (uint32_t *)p;
-#pragma unroll
-    for (int i = 0; i < RS_W; i++) __builtin_nontemporal_store(f[i], q + i);
-}
-
+// 4 pixels of one env and one output stack (blockIdx.y: LoResStack 0 allo / 1 ego; else 0 = past_obs).
+// The ring view of the stack keeps the env's last 4 frames (slot t % 4 = this step); a fresh env (reset,
+// or done = auto-reset) fills every slot with its current frame, as the deques of
+// benchmarks/__init__.py:75-82,139-147 are filled at reset.  Byte work: per env and stack 12 B read (+ 36 B
+// of ring unless fresh), 12 B ring write and 48 B stacked output per 4 pixels -- HBM bound.
 __global__ __launch_bounds__(256) void restack_kernel(const uint8_t *__restrict__ recv, uint32_t world, uint32_t n,
                                                       int64_t stride, int64_t off_a, int64_t off_e, int64_t off_d,
                                                       int32_t preproc, uint32_t slot, int32_t all_fresh,
                                                       uint8_t *__restrict__ ring, uint8_t *__restrict__ out0,
                                                       uint8_t *__restrict__ out1) {
-    constexpr uint32_t Q = LO * LO / RS_PIX;            // threads per env and stack (576)
+    constexpr uint32_t Q = LO * LO / 4;
     const uint32_t W = world * n;
     const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
     const uint32_t g = gid / Q, q = gid - g * Q;
@@ -156,37 +137,39 @@ __global__ __launch_bounds__(256) void restack_kernel(const uint8_t *__restrict_
     const bool fresh = all_fresh || blk[off_d + i] != 0;
     // the view this stack's frames come from (LoRes3EA: ego, with the current allo frame in slot 0)
     const int rv = (preproc == MG_PREPROC_LORES4A || (preproc == MG_PREPROC_LORESSTACK && s == 0)) ? 0 : 1;
-    const size_t po = (size_t)q * (RS_PIX * 3);
+    const size_t po = (size_t)q * 12;
+    const uint32_t *cur = (const uint32_t *)(blk + (rv ? off_e : off_a) + (size_t)i * LOFR + po);
     uint8_t *rring = ring + (size_t)rv * 4 * W * LOFR;
-    auto rslot = [&](uint32_t sl) { return rring + ((size_t)(sl & 3) * W + g) * LOFR + po; };
-    uint32_t f[4][RS_W];
-    ld12(blk + (rv ? off_e : off_a) + (size_t)i * LOFR + po, f[3]);
+    auto rslot = [&](uint32_t sl) { return (uint32_t *)(rring + ((size_t)(sl & 3) * W + g) * LOFR + po); };
+    uint32_t f[4][3];
+#pragma unroll
+    for (int w = 0; w < 3; w++) f[3][w] = cur[w];
     if (fresh) {
 #pragma unroll
         for (int k = 0; k < 3; k++)
 #pragma unroll
-            for (int w = 0; w < RS_W; w++) f[k][w] = f[3][w];
+            for (int w = 0; w < 3; w++) f[k][w] = f[3][w];
 #pragma unroll
-        for (uint32_t sl = 0; sl < 4; sl++) st12_nt(rslot(sl), f[3]);
+        for (uint32_t sl = 0; sl < 4; sl++) {
+            uint32_t *d = rslot(sl);
+            d[0] = f[3][0]; d[1] = f[3][1]; d[2] = f[3][2];
+        }
     } else {
 #pragma unroll
-        for (int k = 0; k < 3; k++) ld12(rslot(slot + 1 + k), f[k]);   // stack slot k = frame t - (3 - k)
-        st12_nt(rslot(slot), f[3]);
-    }
-    if (preproc == MG_PREPROC_LORES3EA)                 // allo depth 1 in front of the ego frames t-2, t-1, t
-        ld12(blk + off_a + (size_t)i * LOFR + po, f[0]);
-    // output: per pixel the 4 frames' 3 bytes, oldest first (48 B per 4 pixels)
-    uint32_t *dst = (uint32_t *)((s ? out1 : out0) + (size_t)g * LOFR * 4 + po * 4);
+        for (int k = 0; k < 3; k++) {          // stack slot k = frame t - (3 - k)
+            const uint32_t *src = rslot(slot + 1 + k);
 #pragma unroll
-    for (int d = 0; d < 4 * RS_W; d++) {                // output dword d: bytes 4d .. 4d + 3
-        uint32_t o = 0;
-#pragma unroll
-        for (int bb = 0; bb < 4; bb++) {
-            const int b = 4 * d + bb, px = b / 12, k = (b % 12) / 3, sb = 3 * px + b % 3;  // source byte in frame k
-            o |= ((f[k][sb / 4] >> (8 * (sb % 4))) & 255u) << (8 * bb);
+            for (int w = 0; w < 3; w++) f[k][w] = src[w];
         }
-        __builtin_nontemporal_store(o, dst + d);
+        uint32_t *d = rslot(slot);
+        d[0] = f[3][0]; d[1] = f[3][1]; d[2] = f[3][2];
     }
+    if (preproc == MG_PREPROC_LORES3EA) {      // allo depth 1 in front of the ego frames t-2, t-1, t
+        const uint32_t *a = (const uint32_t *)(blk + off_a + (size_t)i * LOFR + po);
+#pragma unroll
+        for (int w = 0; w < 3; w++) f[0][w] = a[w];
+    }
+    stack_regs(f, (s ? out1 : out0) + (size_t)g * LOFR * 4 + po * 4);
 }
 }  // namespace
 
@@ -210,7 +193,7 @@ extern "C" hipError_t mg_launch_restack(const uint8_t *recv, int32_t world, int3
                                         int64_t off_e, int64_t off_d, int32_t preproc, int64_t step, int32_t all_fresh,
                                         uint8_t *ring, uint8_t *out_allo, uint8_t *out_ego, uint8_t *out_past,
                                         hipStream_t st) {
-    const int64_t t = (int64_t)world * n * (LO * LO / RS_PIX);
+    const int64_t t = (int64_t)world * n * (LO * LO / 4);
     const bool two = preproc == MG_PREPROC_LORESSTACK;
     hipLaunchKernelGGL(restack_kernel, dim3((unsigned)((t + 255) / 256), two ? 2 : 1), dim3(256), 0, st, recv,
                        (uint32_t)world, (uint32_t)n, stride, off_a, off_e, off_d, preproc, (uint32_t)(step & 3),

@@ -9,7 +9,8 @@
 // drawn in the reference's order so parity mode replays the reference stream.
 #pragma once
 #include "mg_launch.h"
-#include "mg_step.h"
+#include "mg_phys.h"
+#include "mg_prof.h"
 
 #define MT(i) S.mt_key[(size_t)(i) * (size_t)S.N + (size_t)e]
 

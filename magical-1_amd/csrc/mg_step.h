@@ -365,34 +365,6 @@ struct RegCons {
         wcoef;
 };
 
-template <int NB>
-MG_DEV double rsel(const double (&x)[NB], int b) {
-    double r = 0.0;
-#pragma unroll
-    for (int k = 0; k < NB; k++) r = b == k ? x[k] : r;
-    return r;
-}
-template <int NB>
-MG_DEV void rput(double (&x)[NB], int b, double v) {
-#pragma unroll
-    for (int k = 0; k < NB; k++) x[k] = b == k ? v : x[k];
-}
-
-// runtime body slot (arbiters)
-template <int NB>
-MG_DEV void rapply_dyn(RegBodies<NB> &R, int b, double minv, double iinv, V2 j, V2 r) {
-    if (b < 0) return;
-    rput(R.vx, b, rsel(R.vx, b) + j.x * minv);
-    rput(R.vy, b, rsel(R.vy, b) + j.y * minv);
-    rput(R.w, b, rsel(R.w, b) + iinv * vcross(r, j));
-}
-template <int NB>
-MG_DEV void rapply_bias_dyn(RegBodies<NB> &R, int b, double minv, double iinv, V2 j, V2 r) {
-    if (b < 0) return;
-    rput(R.vbx, b, rsel(R.vbx, b) + j.x * minv);
-    rput(R.vby, b, rsel(R.vby, b) + j.y * minv);
-    rput(R.wb, b, rsel(R.wb, b) + iinv * vcross(r, j));
-}
 // compile-time body slot (constraints; b < 0 = the static body)
 template <int NB>
 MG_DEV void rapply(RegBodies<NB> &R, int b, V2 j, V2 r) {
@@ -533,34 +505,82 @@ MG_DEV void rcons_apply(RegBodies<NB> &R, RegCons &q, int a, int b, int type) {
     }
 }
 
+// Arbiter body slots of the compile-time scenes: only the bodies that carry shapes (robot 0, fingers 4-5,
+// block 6) can be in contact, so a runtime slot is a one-hot over those (all false: the static body) and
+// reads / writes select among 3-4 registers instead of all NB (the step kernel checks that every shape
+// of such a scene is on one of those bodies).
+__host__ __device__ constexpr bool shape_body_slot(int k) { return k == 0 || k == 4 || k == 5 || k == 6; }
 template <int NB>
-MG_DEV void rarb_cached(RegBodies<NB> &R, const MGState &S, int e, int slot, double dt_coef) {
+struct ArbBody { bool m[NB]; };
+template <int NB>
+MG_DEV ArbBody<NB> arb_body(int b) {
+    ArbBody<NB> h;
+#pragma unroll
+    for (int k = 0; k < NB; k++) h.m[k] = shape_body_slot(k) && b == k;
+    return h;
+}
+template <int NB>
+MG_DEV double hsel(const double (&x)[NB], const ArbBody<NB> &h) {
+    double r = 0.0;
+#pragma unroll
+    for (int k = 0; k < NB; k++)
+        if (shape_body_slot(k)) r = h.m[k] ? x[k] : r;
+    return r;
+}
+template <int NB>
+MG_DEV void hput(double (&x)[NB], const ArbBody<NB> &h, double v) {
+#pragma unroll
+    for (int k = 0; k < NB; k++)
+        if (shape_body_slot(k)) x[k] = h.m[k] ? v : x[k];
+}
+template <int NB>
+MG_DEV void happly(RegBodies<NB> &R, const ArbBody<NB> &h, double minv, double iinv, V2 j, V2 r) {
+    hput(R.vx, h, hsel(R.vx, h) + j.x * minv);
+    hput(R.vy, h, hsel(R.vy, h) + j.y * minv);
+    hput(R.w, h, hsel(R.w, h) + iinv * vcross(r, j));
+}
+template <int NB>
+MG_DEV void happly_bias(RegBodies<NB> &R, const ArbBody<NB> &h, double minv, double iinv, V2 j, V2 r) {
+    hput(R.vbx, h, hsel(R.vbx, h) + j.x * minv);
+    hput(R.vby, h, hsel(R.vby, h) + j.y * minv);
+    hput(R.wb, h, hsel(R.wb, h) + iinv * vcross(r, j));
+}
+template <int NB>
+MG_DEV void harb_cached(RegBodies<NB> &R, const MGState &S, int e, int slot, double dt_coef) {
     if (AT(S.astate, slot) == ARB_FIRST) return;
-    const int a = AT(S.asa, slot), b = AT(S.asb, slot);
-    const double am = rsel(R.minv, a), ai = rsel(R.iinv, a), bm = rsel(R.minv, b), bi = rsel(R.iinv, b);
+    const ArbBody<NB> ha = arb_body<NB>(AT(S.asa, slot)), hb = arb_body<NB>(AT(S.asb, slot));
+    const double am = hsel(R.minv, ha), ai = hsel(R.iinv, ha), bm = hsel(R.minv, hb), bi = hsel(R.iinv, hb);
     V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
     int cnt = AT(S.acount, slot);
     for (int k = 0; k < cnt; k++) {
         V2 j = vmult(vrotate(n, v2(ACON(k, AC_JN, slot), ACON(k, AC_JT, slot))), dt_coef);
-        rapply_dyn(R, a, am, ai, vneg(j), v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)));
-        rapply_dyn(R, b, bm, bi, j, v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot)));
+        happly(R, ha, am, ai, vneg(j), v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)));
+        happly(R, hb, bm, bi, j, v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot)));
     }
 }
-
 template <int NB>
-MG_DEV void rarb_apply(RegBodies<NB> &R, const MGState &S, int e, int slot) {
-    const int a = AT(S.asa, slot), b = AT(S.asb, slot);
-    const double am = rsel(R.minv, a), ai = rsel(R.iinv, a), bm = rsel(R.minv, b), bi = rsel(R.iinv, b);
+MG_DEV void harb_apply(RegBodies<NB> &R, const MGState &S, int e, int slot) {
+    const int sa = AT(S.asa, slot), sb = AT(S.asb, slot);
+    const ArbBody<NB> ha = arb_body<NB>(sa), hb = arb_body<NB>(sb);
+    const double am = hsel(R.minv, ha), ai = hsel(R.iinv, ha), bm = hsel(R.minv, hb), bi = hsel(R.iinv, hb);
+    // a side whose body is static in every lane running this row (a wall: velocity +0.0 exactly, impulses
+    // applied to nothing) skips its selects -- a wave-uniform branch
+    const bool wa = __ballot(sa >= 0) != 0, wb = __ballot(sb >= 0) != 0;
     V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
     double friction = AT(S.au, slot);
     int cnt = AT(S.acount, slot);
     for (int k = 0; k < cnt; k++) {
         double nMass = ACON(k, AC_NMASS, slot);
         V2 r1 = v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)), r2 = v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot));
-        V2 vb1 = vadd(v2(rsel(R.vbx, a), rsel(R.vby, a)), vmult(vperp(r1), rsel(R.wb, a)));
-        V2 vb2 = vadd(v2(rsel(R.vbx, b), rsel(R.vby, b)), vmult(vperp(r2), rsel(R.wb, b)));
-        V2 v1 = vadd(v2(rsel(R.vx, a), rsel(R.vy, a)), vmult(vperp(r1), rsel(R.w, a)));
-        V2 v2_ = vadd(v2(rsel(R.vx, b), rsel(R.vy, b)), vmult(vperp(r2), rsel(R.w, b)));
+        V2 vb1 = v2(0.0, 0.0), v1 = v2(0.0, 0.0), vb2 = v2(0.0, 0.0), v2_ = v2(0.0, 0.0);
+        if (wa) {
+            vb1 = vadd(v2(hsel(R.vbx, ha), hsel(R.vby, ha)), vmult(vperp(r1), hsel(R.wb, ha)));
+            v1 = vadd(v2(hsel(R.vx, ha), hsel(R.vy, ha)), vmult(vperp(r1), hsel(R.w, ha)));
+        }
+        if (wb) {
+            vb2 = vadd(v2(hsel(R.vbx, hb), hsel(R.vby, hb)), vmult(vperp(r2), hsel(R.wb, hb)));
+            v2_ = vadd(v2(hsel(R.vx, hb), hsel(R.vy, hb)), vmult(vperp(r2), hsel(R.w, hb)));
+        }
         V2 vr = vsub(v2_, v1);
         double vbn = vdot(vsub(vb2, vb1), n);
         double vrn = vdot(vr, n);
@@ -579,11 +599,11 @@ MG_DEV void rarb_apply(RegBodies<NB> &R, const MGState &S, int e, int slot) {
         double jtAcc = cpclamp(jtOld + jt, -jtMax, jtMax);
         ACON(k, AC_JT, slot) = jtAcc;
         V2 jb = vmult(n, jBias - jbnOld);
-        rapply_bias_dyn(R, a, am, ai, vneg(jb), r1);
-        rapply_bias_dyn(R, b, bm, bi, jb, r2);
+        if (wa) happly_bias(R, ha, am, ai, vneg(jb), r1);
+        if (wb) happly_bias(R, hb, bm, bi, jb, r2);
         V2 j = vrotate(n, v2(jnAcc - jnOld, jtAcc - jtOld));
-        rapply_dyn(R, a, am, ai, vneg(j), r1);
-        rapply_dyn(R, b, bm, bi, j, r2);
+        if (wa) happly(R, ha, am, ai, vneg(j), r1);
+        if (wb) happly(R, hb, bm, bi, j, r2);
     }
 }
 
@@ -629,12 +649,18 @@ MG_DEV void static_solve(const MGState &S, int e, double dt, double dt_coef, int
     RegCons q[NCS];
     rb_load(R, S, e);
     rstatic_load<NCS>(q, S, e, dt);
-    for (int i = 0; i < nact; i++) rarb_cached(R, S, e, AT(S.active, i), dt_coef);
+    for (int i = 0; i < nact; i++) harb_cached(R, S, e, AT(S.active, i), dt_coef);
     rstatic_cached<NCS>(R, q, dt_coef);
     MG_PP(P, 5);
+#ifndef MG_EXP_ITERS        // timing experiments only (tools/build_unit_variant.sh)
+#define MG_EXP_ITERS 10
+#endif
+#ifdef MG_EXP_NOARBIT       // timing experiments only: no arbiter rows in the iterations
+    nact = 0;
+#endif
 #pragma unroll 1
-    for (int it = 0; it < 10; it++) {
-        for (int i = 0; i < nact; i++) rarb_apply(R, S, e, AT(S.active, i));
+    for (int it = 0; it < MG_EXP_ITERS; it++) {
+        for (int i = 0; i < nact; i++) harb_apply(R, S, e, AT(S.active, i));
         rstatic_apply<NCS>(R, q);
     }
     rb_store(R, S, e);
@@ -669,6 +695,9 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
     constexpr bool LDS_SHAPES = NCS > 0 && step_variant_caps(NCS == 10 ? 1 : 2).shw > 0;
     ShapeW &A = LDS_SHAPES ? S.shw[3 * e] : locA, &W = LDS_SHAPES ? S.shw[3 * e + 1] : locW;
     ShapeW &B = LDS_SHAPES ? S.shw[3 * e + 2] : locB;
+#ifdef MG_EXP_NO_NARROW     // timing experiments only (tools/build_unit_variant.sh): no collisions at all
+    ns = 0;
+#endif
     for (int i = 0; i < ns; i++) {
         // BB tests on the cached BBs; the world-space shape is built only for pairs that pass
         const double al = AT(S.sbbl, i), ab = AT(S.sbbb, i), ar = AT(S.sbbr, i), at = AT(S.sbbt, i);
@@ -997,6 +1026,211 @@ MG_DEV void lground_apply(LaneBodies &R, const MGState &S, int e, int c, double 
     }
 }
 
+// Robot rows of the cooperative sweep on wave-uniform registers.  One env per wavefront: the robot's six
+// bodies (rb0 .. rb0 + 5) and its ten joints' terms live in every lane's registers as in static_solve, so
+// the robot rows (3/4 of the sweep's time when read through readlane / lane-select) index bodies by
+// constants; block bodies stay in their lanes; arbiter rows reach a robot body through a uniform select.
+// Same operations in the same order as lcons_* / larb_*.
+MG_DEV double uget6(const double (&x)[6], int k) {
+    double r = x[0];
+#pragma unroll
+    for (int i = 1; i < 6; i++) r = k == i ? x[i] : r;
+    return r;
+}
+MG_DEV void uput6(double (&x)[6], int k, double v) {
+#pragma unroll
+    for (int i = 0; i < 6; i++) x[i] = k == i ? v : x[i];
+}
+MG_DEV bool is_rob(int b, int rb0) { return b >= rb0 && b < rb0 + 6; }
+// the robot's velocities, masses and joint accumulators (wave-uniform); the bias velocities (touched by
+// arbiter rows only) stay in the bodies' lanes
+struct RobotV { double vx[6], vy[6], w[6], minv[6], iinv[6], jacc[10], jacc2[10], twrn[10]; };
+MG_DEV double xget(double lf, const double (&rf)[6], int b, int rb0) {
+    if (b < 0) return 0.0;
+    if (is_rob(b, rb0)) return uget6(rf, b - rb0);
+    return rl_d(lf, b);
+}
+MG_DEV void xput(double &lf, double (&rf)[6], int b, int rb0, int lane, double v) {
+    if (b < 0) return;
+    if (is_rob(b, rb0)) uput6(rf, b - rb0, v);
+    else lput(lf, b, lane, v);
+}
+MG_DEV void xapply(LaneBodies &R, RobotV &V, int rb0, int lane, int b, V2 j, V2 r) {
+    if (b < 0) return;
+    const double minv = xget(R.minv, V.minv, b, rb0), iinv = xget(R.iinv, V.iinv, b, rb0);
+    xput(R.vx, V.vx, b, rb0, lane, xget(R.vx, V.vx, b, rb0) + j.x * minv);
+    xput(R.vy, V.vy, b, rb0, lane, xget(R.vy, V.vy, b, rb0) + j.y * minv);
+    xput(R.w, V.w, b, rb0, lane, xget(R.w, V.w, b, rb0) + iinv * vcross(r, j));
+}
+MG_DEV void xapply_bias(LaneBodies &R, RobotV &V, int rb0, int lane, int b, V2 j, V2 r) {
+    if (b < 0) return;
+    const double minv = xget(R.minv, V.minv, b, rb0), iinv = xget(R.iinv, V.iinv, b, rb0);
+    lput(R.vbx, b, lane, lget(R.vbx, b) + j.x * minv);
+    lput(R.vby, b, lane, lget(R.vby, b) + j.y * minv);
+    lput(R.wb, b, lane, lget(R.wb, b) + iinv * vcross(r, j));
+}
+MG_DEV void xarb_cached(LaneBodies &R, RobotV &V, int rb0, int lane, const MGState &S, int e, int slot,
+                        double dt_coef) {
+    if (ufirst(AT(S.astate, slot)) == ARB_FIRST) return;
+    const int a = ufirst(AT(S.asa, slot)), b = ufirst(AT(S.asb, slot));
+    V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
+    const int cnt = ufirst(AT(S.acount, slot));
+    for (int k = 0; k < cnt; k++) {
+        V2 j = vmult(vrotate(n, v2(ACON(k, AC_JN, slot), ACON(k, AC_JT, slot))), dt_coef);
+        xapply(R, V, rb0, lane, a, vneg(j), v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)));
+        xapply(R, V, rb0, lane, b, j, v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot)));
+    }
+}
+MG_DEV void xarb_apply(LaneBodies &R, RobotV &V, int rb0, int lane, const MGState &S, int e, int slot) {
+    const int a = ufirst(AT(S.asa, slot)), b = ufirst(AT(S.asb, slot));
+    V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
+    double friction = AT(S.au, slot);
+    const int cnt = ufirst(AT(S.acount, slot));
+    for (int k = 0; k < cnt; k++) {
+        double nMass = ACON(k, AC_NMASS, slot);
+        V2 r1 = v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)), r2 = v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot));
+        V2 vb1 = vadd(v2(lget(R.vbx, a), lget(R.vby, a)), vmult(vperp(r1), lget(R.wb, a)));
+        V2 vb2 = vadd(v2(lget(R.vbx, b), lget(R.vby, b)), vmult(vperp(r2), lget(R.wb, b)));
+        V2 v1 = vadd(v2(xget(R.vx, V.vx, a, rb0), xget(R.vy, V.vy, a, rb0)), vmult(vperp(r1), xget(R.w, V.w, a, rb0)));
+        V2 v2_ = vadd(v2(xget(R.vx, V.vx, b, rb0), xget(R.vy, V.vy, b, rb0)), vmult(vperp(r2), xget(R.w, V.w, b, rb0)));
+        V2 vr = vsub(v2_, v1);
+        double vbn = vdot(vsub(vb2, vb1), n);
+        double vrn = vdot(vr, n);
+        double vrt = vdot(vr, vperp(n));
+        double jbn = (ACON(k, AC_BIAS, slot) - vbn) * nMass;
+        double jbnOld = ACON(k, AC_JB, slot);
+        double jBias = cpmax(jbnOld + jbn, 0.0);
+        double jn = -(0.0 + vrn) * nMass;
+        double jnOld = ACON(k, AC_JN, slot);
+        double jnAcc = cpmax(jnOld + jn, 0.0);
+        double jtMax = friction * jnAcc;
+        double jt = -vrt * ACON(k, AC_TMASS, slot);
+        double jtOld = ACON(k, AC_JT, slot);
+        double jtAcc = cpclamp(jtOld + jt, -jtMax, jtMax);
+        if (lane == 0) { ACON(k, AC_JB, slot) = jBias; ACON(k, AC_JN, slot) = jnAcc; ACON(k, AC_JT, slot) = jtAcc; }
+        V2 jb = vmult(n, jBias - jbnOld);
+        xapply_bias(R, V, rb0, lane, a, vneg(jb), r1);
+        xapply_bias(R, V, rb0, lane, b, jb, r2);
+        V2 j = vrotate(n, v2(jnAcc - jnOld, jtAcc - jtOld));
+        xapply(R, V, rb0, lane, a, vneg(j), r1);
+        xapply(R, V, rb0, lane, b, j, r2);
+    }
+}
+// robot joint K (static_cons(K): compile-time type and body slots) at list index c: lcons_cached /
+// lcons_apply with the bodies and accumulators in registers and the pre-stepped terms read from LDS
+template <int K>
+MG_DEV void rrow_apply(RobotV &V, const MGState &S, int e, int c, double dt) {
+    constexpr ConsDesc d = static_cons(K);
+    constexpr int a = d.a, b = d.b;
+    if constexpr (d.type == MG_C_PIVOT) {
+        V2 r1 = v2(CPA(CP_R1X, c), CPA(CP_R1Y, c)), r2 = v2(CPA(CP_R2X, c), CPA(CP_R2Y, c));
+        V2 v1 = vadd(v2(V.vx[a], V.vy[a]), vmult(vperp(r1), V.w[a]));
+        V2 v2_ = vadd(v2(V.vx[b], V.vy[b]), vmult(vperp(r2), V.w[b]));
+        V2 vr = vsub(v2_, v1);
+        V2 dd = vsub(v2(CPA(CP_BIAS, c), CPA(CP_BIAS2, c)), vr);
+        V2 j = v2(dd.x * CPA(CP_K11, c) + dd.y * CPA(CP_K12, c), dd.x * CPA(CP_K21, c) + dd.y * CPA(CP_K22, c));
+        V2 jOld = v2(V.jacc[K], V.jacc2[K]);
+        V2 jAcc = vclamp(vadd(jOld, j), CPA(CP_MAXF, c) * dt);
+        V.jacc[K] = jAcc.x; V.jacc2[K] = jAcc.y;
+        V2 dj = vsub(jAcc, jOld);
+        const V2 ja = vneg(dj);
+        V.vx[a] = V.vx[a] + ja.x * V.minv[a]; V.vy[a] = V.vy[a] + ja.y * V.minv[a];
+        V.w[a] = V.w[a] + V.iinv[a] * vcross(r1, ja);
+        V.vx[b] = V.vx[b] + dj.x * V.minv[b]; V.vy[b] = V.vy[b] + dj.y * V.minv[b];
+        V.w[b] = V.w[b] + V.iinv[b] * vcross(r2, dj);
+    } else if constexpr (d.type == MG_C_GEAR) {
+        double ratio = CPA(CP_RATIO, c);
+        double wr = V.w[b] * ratio - V.w[a];
+        double jMax = CPA(CP_MAXF, c) * dt;
+        double j = (CPA(CP_BIAS, c) - wr) * CPA(CP_ISUM, c);
+        double jOld = V.jacc[K];
+        double jAcc = cpclamp(jOld + j, -jMax, jMax);
+        V.jacc[K] = jAcc;
+        j = jAcc - jOld;
+        V.w[a] = V.w[a] - j * V.iinv[a] * CPA(CP_RATIO_INV, c);
+        V.w[b] = V.w[b] + j * V.iinv[b];
+    } else if constexpr (d.type == MG_C_ROTLIMIT) {
+        double bias = CPA(CP_BIAS, c);
+        if (!bias) return;
+        double wr = V.w[b] - V.w[a];
+        double jMax = CPA(CP_MAXF, c) * dt;
+        double j = -(bias + wr) * CPA(CP_ISUM, c);
+        double jOld = V.jacc[K];
+        double jAcc = bias < 0.0 ? cpclamp(jOld + j, 0.0, jMax) : cpclamp(jOld + j, -jMax, 0.0);
+        V.jacc[K] = jAcc;
+        j = jAcc - jOld;
+        V.w[a] = V.w[a] - j * V.iinv[a];
+        V.w[b] = V.w[b] + j * V.iinv[b];
+    } else if constexpr (d.type == MG_C_MOTOR) {
+        double wr = V.w[b] - V.w[a] + CPA(CP_RATE, c);
+        double jMax = CPA(CP_MAXF, c) * dt;
+        double j = -wr * CPA(CP_ISUM, c);
+        double jOld = V.jacc[K];
+        double jAcc = cpclamp(jOld + j, -jMax, jMax);
+        V.jacc[K] = jAcc;
+        j = jAcc - jOld;
+        V.w[a] = V.w[a] - j * V.iinv[a];
+        V.w[b] = V.w[b] + j * V.iinv[b];
+    } else if constexpr (d.type == MG_C_SPRING) {
+        double wrn = V.w[a] - V.w[b];
+        double w_damp = (V.twrn[K] - wrn) * CPA(CP_WCOEF, c);
+        V.twrn[K] = wrn + w_damp;
+        double j_damp = w_damp * CPA(CP_ISUM, c);
+        V.jacc[K] = V.jacc[K] + j_damp;
+        V.w[a] = V.w[a] + j_damp * V.iinv[a];
+        V.w[b] = V.w[b] - j_damp * V.iinv[b];
+    }
+}
+template <int K>
+MG_DEV void rrow_cached(RobotV &V, const MGState &S, int e, int c, double dt_coef) {
+    constexpr ConsDesc d = static_cons(K);
+    constexpr int a = d.a, b = d.b;
+    if constexpr (d.type == MG_C_PIVOT) {
+        V2 j = vmult(v2(V.jacc[K], V.jacc2[K]), dt_coef);
+        const V2 r1 = v2(CPA(CP_R1X, c), CPA(CP_R1Y, c)), r2 = v2(CPA(CP_R2X, c), CPA(CP_R2Y, c));
+        const V2 ja = vneg(j);
+        V.vx[a] = V.vx[a] + ja.x * V.minv[a]; V.vy[a] = V.vy[a] + ja.y * V.minv[a];
+        V.w[a] = V.w[a] + V.iinv[a] * vcross(r1, ja);
+        V.vx[b] = V.vx[b] + j.x * V.minv[b]; V.vy[b] = V.vy[b] + j.y * V.minv[b];
+        V.w[b] = V.w[b] + V.iinv[b] * vcross(r2, j);
+    } else if constexpr (d.type == MG_C_GEAR) {
+        double j = V.jacc[K] * dt_coef;
+        V.w[a] = V.w[a] - j * V.iinv[a] * CPA(CP_RATIO_INV, c);
+        V.w[b] = V.w[b] + j * V.iinv[b];
+    } else if constexpr (d.type == MG_C_ROTLIMIT || d.type == MG_C_MOTOR) {
+        double j = V.jacc[K] * dt_coef;
+        V.w[a] = V.w[a] - j * V.iinv[a];
+        V.w[b] = V.w[b] + j * V.iinv[b];
+    }
+}
+template <int K = 0>
+MG_DEV void rrows_cached(RobotV &V, const MGState &S, int e, int rc0, double dt_coef) {
+    if constexpr (K < 10) { rrow_cached<K>(V, S, e, rc0 + K, dt_coef); rrows_cached<K + 1>(V, S, e, rc0, dt_coef); }
+}
+template <int K = 0>
+MG_DEV void rrows_apply(RobotV &V, const MGState &S, int e, int rc0, double dt) {
+    if constexpr (K < 10) { rrow_apply<K>(V, S, e, rc0 + K, dt); rrows_apply<K + 1>(V, S, e, rc0, dt); }
+}
+
+// the env's constraint list is the blocks' ground rows (G) plus the robot's ten joints at rc0 in
+// static_cons order on bodies rb0 + slot: the robot rows can run on registers
+MG_DEV bool robot_rows_static(const MGState &S, int e, const GroundRows &G, int unc, int rb0, int rc0) {
+    if (rb0 < 0 || rc0 < 0 || rc0 + 10 > unc) return false;
+    bool ok = true;
+    // static_cons is indexed by compile-time constants only (a runtime index into its local table could be
+    // speculated out of range)
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+        const ConsDesc d = static_cons(k);
+        const int c = rc0 + k;
+        ok = ok && ufirst(AT(S.ctype, c)) == d.type && ufirst(AT(S.ca, c)) == rb0 + d.a &&
+             ufirst(AT(S.cb, c)) == rb0 + d.b;
+    }
+    for (int c = 0; c < unc; c++)
+        if (c < rc0 || c >= rc0 + 10) ok = ok && is_ground_row(G, ufirst(AT(S.cb, c)));
+    return ok;
+}
+
 MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, int lane, MGProf &P) {
     const int e = 0;
     const uint32_t stamp = S.stamp[e] + 1;
@@ -1127,6 +1361,59 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
     const double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
     const int unact = ufirst(nact), unc = ufirst(nc);
     const GroundRows G = ground_rows(S, e, lane, nb, nc);
+#ifndef MG_EXP_COOP_NORR   // timing experiments only: the lane-select robot rows below
+    const int rb0 = ufirst(S.robot_body0[e]), rc0 = ufirst(S.robot_cons0[e]);
+    if (robot_rows_static(S, e, G, unc, rb0, rc0)) {
+        RobotV V;
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const int b = rb0 + k;
+            V.vx[k] = AT(S.bvx, b); V.vy[k] = AT(S.bvy, b); V.w[k] = AT(S.bw, b);
+            V.minv[k] = AT(S.bminv, b); V.iinv[k] = AT(S.biinv, b);
+        }
+#pragma unroll
+        for (int k = 0; k < 10; k++) {
+            V.jacc[k] = CPA(CP_JACC, rc0 + k);
+            V.jacc2[k] = static_cons(k).type == MG_C_PIVOT ? CPA(CP_JACC2, rc0 + k) : 0.0;
+            V.twrn[k] = static_cons(k).type == MG_C_SPRING ? CPA(CP_TWRN, rc0 + k) : 0.0;
+        }
+        for (int i = 0; i < unact; i++) xarb_cached(R, V, rb0, lane, S, e, ufirst(AT(S.active, i)), dt_coef);
+        if (G.n > 0) {
+            lground_cached(R, S, e, G.c0, dt_coef);
+            if (G.n > 1) lground_cached(R, S, e, G.c1, dt_coef);
+        }
+        rrows_cached(V, S, e, rc0, dt_coef);
+        MG_PP(P, 5);
+#pragma unroll 1
+        for (int it = 0; it < 10; it++) {
+            for (int i = 0; i < unact; i++) xarb_apply(R, V, rb0, lane, S, e, ufirst(AT(S.active, i)));
+            if (G.n > 0) {
+                lground_apply(R, S, e, G.c0, dt);
+                if (G.n > 1) lground_apply(R, S, e, G.c1, dt);
+            }
+            rrows_apply(V, S, e, rc0, dt);
+        }
+        // robot lanes: velocities from V (their bias velocities stayed in the lanes)
+        if (lane < nb) {
+            const bool rob = is_rob(lane, rb0);
+            const int k = rob ? lane - rb0 : 0;
+            AT(S.bvx, lane) = rob ? uget6(V.vx, k) : R.vx; AT(S.bvy, lane) = rob ? uget6(V.vy, k) : R.vy;
+            AT(S.bw, lane) = rob ? uget6(V.w, k) : R.w;
+            AT(S.bvbx, lane) = R.vbx; AT(S.bvby, lane) = R.vby; AT(S.bwb, lane) = R.wb;
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 10; k++) {
+                CPA(CP_JACC, rc0 + k) = V.jacc[k];
+                if (static_cons(k).type == MG_C_PIVOT) CPA(CP_JACC2, rc0 + k) = V.jacc2[k];
+                if (static_cons(k).type == MG_C_SPRING) CPA(CP_TWRN, rc0 + k) = V.twrn[k];
+            }
+        }
+        MG_PP(P, 6);
+        __syncthreads();
+        return;
+    }
+#endif
     for (int i = 0; i < unact; i++) larb_cached(R, lane, S, e, ufirst(AT(S.active, i)), dt_coef);
     if (G.n > 0) {
         lground_cached(R, S, e, G.c0, dt_coef);
@@ -1138,18 +1425,25 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
         lcons_cached(R, lane, S, e, c, ufirst(AT(S.ca, c)), cb, ufirst(AT(S.ctype, c)), dt_coef);
     }
     MG_PP(P, 5);
+#ifndef MG_EXP_COOP_ITERS   // timing experiments only (tools/build_unit_variant.sh)
+#define MG_EXP_COOP_ITERS 10
+#endif
 #pragma unroll 1
-    for (int it = 0; it < 10; it++) {
+    for (int it = 0; it < MG_EXP_COOP_ITERS; it++) {
+#ifndef MG_EXP_COOP_NOARB
         for (int i = 0; i < unact; i++) larb_apply(R, lane, S, e, ufirst(AT(S.active, i)));
+#endif
         if (G.n > 0) {
             lground_apply(R, S, e, G.c0, dt);
             if (G.n > 1) lground_apply(R, S, e, G.c1, dt);
         }
+#ifndef MG_EXP_COOP_NOCONS
         for (int c = 0; c < unc; c++) {
             const int cb = ufirst(AT(S.cb, c));
             if (is_ground_row(G, cb)) continue;
             lcons_apply(R, lane, S, e, c, ufirst(AT(S.ca, c)), cb, ufirst(AT(S.ctype, c)), dt);
         }
+#endif
     }
     if (lane < nb) {
         AT(S.bvx, lane) = R.vx; AT(S.bvy, lane) = R.vy; AT(S.bw, lane) = R.w;

@@ -4,6 +4,7 @@
 // mg_physics.hip dispatches.
 #pragma once
 #include "mg_launch.h"
+#include "mg_step.h"
 #include "mg_score.h"
 
 // ---- LDS-resident substeps ------------------------------------------------
@@ -183,6 +184,7 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
             const ConsDesc d = static_cons(c);
             ok = ok && AT(S.ctype, c) == d.type && AT(S.ca, c) == d.a && AT(S.cb, c) == d.b;
         }
+        for (int k = 0; k < S.nshapes[e] && NCS > 0; k++) ok = ok && shape_body_slot(AT(S.sbody, k)); // arb_body
         if (!ok) { // the compiled constraint list does not describe this scene (never expected)
             S.overflow[e] |= 32;
             if (reset_mask) reset_mask[e] = 0;

@@ -22,7 +22,7 @@ _STEP = _PHYS + ["mg_reset.h", "mg_score.h", "mg_stepk.h"]
 UNITS = {  # translation unit -> headers it depends on (one unit per kernel family: they compile in parallel)
     "mg_sim.hip": _COMMON + ["mg_phys.h"],
     "mg_physics.hip": _COMMON + ["mg_phys.h"],
-    "mg_reset.hip": _PHYS + ["mg_reset.h"],
+    "mg_reset.hip": _COMMON + ["mg_phys.h", "mg_reset.h"],
     "mg_step_robot.hip": _STEP,
     "mg_step_v3.hip": _STEP,
     "mg_step_v4.hip": _STEP,

@@ -337,23 +337,30 @@ def test_full_resolution_frames(name, retry, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,n,steps", [("MoveToRegion-Demo-LoRes4E-v0", 1, 200),
-                                          ("MoveToRegion-Demo-LoRes4E-v0", 4096, 205),
-                                          ("MoveToCorner-Demo-LoRes4E-v0", 4096, 85),
-                                          ("ClusterColour-Demo-LoResStack-v0", 8192, 50),
-                                          ("MatchRegions-TestAll-LoRes4E-v0", 8192, 125)])
-def test_full_size_sampled_parity(name, n, steps):
+@pytest.mark.parametrize("name,n,steps,L", [("MoveToRegion-Demo-LoRes4E-v0", 1, 200, None),
+                                            ("MoveToRegion-Demo-LoRes4E-v0", 4096, 205, None),
+                                            ("MoveToRegion-Demo-LoRes4E-v0", 4096, 210, 250),
+                                            ("MoveToCorner-Demo-LoRes4E-v0", 4096, 85, None),
+                                            ("MoveToCorner-Demo-LoRes4E-v0", 4096, 210, 250),
+                                            ("ClusterColour-Demo-LoResStack-v0", 64, 255, None),
+                                            ("ClusterColour-Demo-LoResStack-v0", 8192, 250, None),
+                                            ("MatchRegions-TestAll-LoRes4E-v0", 8192, 125, None)])
+def test_full_size_sampled_parity(name, n, steps, L):
     """BASELINE configs at their sizes (C2 4096, C3 4096, C4 8192, C5 8192) plus the C1 plumbing case
     (1 env x 200 steps): every env steps on the GPU, a spread of envs (incl. the first/last lanes of
-    64-wide blocks and the last env) is checked against the oracle every step -- observations
-    bit-exact, body state (p, a, v, w) within POSE_TOL (north star: positions within 1e-4 over 200
-    steps), done / eval_score equal -- across auto-reset boundaries (MoveToRegion: 5 episodes of 40,
-    MoveToCorner 80, ClusterColour 80 and MatchRegions 120 steps)."""
+    64-wide blocks and the last env; every env when n <= 64) is checked against the oracle every step --
+    observations bit-exact, body state (p, a, v, w) within POSE_TOL (north star: positions within 1e-4
+    over 200 steps), done / eval_score equal.  Episode lengths: MoveToRegion 40, MoveToCorner 80,
+    ClusterColour 240, MatchRegions 120 steps, so the default cases cross 5 / 1 / 1 / 1 auto-resets
+    (ClusterColour-Demo-LoResStack at step 240, with its frame stacks refilled); L = 250 lifts the
+    TimeLimit so MoveToRegion / MoveToCorner run 210 contiguous physics steps with no reset."""
     spec = registry.lookup(name)
     seeds = [1000 + i for i in range(n)]
-    vec = magical_amd.make_vec(name, n, seeds=seeds)
-    pick = sorted(i for i in {0, 1, 63, 64, 127, n // 2 + 5, n - 65, n - 1} if 0 <= i < n)
-    orc = {i: oracle_env(spec, seeds[i]) for i in pick}
+    vec = magical_amd.make_vec(name, n, seeds=seeds, max_episode_steps=L)
+    pick = list(range(n)) if n <= 64 else sorted(i for i in {0, 1, 63, 64, 127, n // 2 + 5, n - 65, n - 1} if 0 <= i < n)
+    orc = {i: po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, L or spec.max_episode_steps, seed=seeds[i])
+           for i in pick}
+    resets = 0
     acts = np.random.RandomState(9).randint(0, 18, (steps, n))
     obs = vec.reset()
     for i in pick:
@@ -371,6 +378,7 @@ def test_full_size_sampled_parity(name, n, steps):
             assert bool(got_done[j]) == d and got_score[j] == s, f"step {t} env {i}"
             if d:
                 o = orc[i].reset()
+                resets += 1
             else:
                 b = orc[i].bodies()
                 diff = np.abs(bodies[j, :len(b)] - b).max()
@@ -378,6 +386,7 @@ def test_full_size_sampled_parity(name, n, steps):
             ref = oracle_obs_split(spec, o)
             for k in got:
                 assert np.array_equal(got[k][j], ref[k]), f"step {t} env {i} obs {k}"
+    assert resets == len(pick) * (steps // (L or spec.max_episode_steps))
     assert int(vec.errors().abs().sum().item()) == 0
     vec.close()
 
