@@ -1361,6 +1361,9 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
     const double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
     const int unact = ufirst(nact), unc = ufirst(nc);
     const GroundRows G = ground_rows(S, e, lane, nb, nc);
+#ifndef MG_EXP_COOP_ITERS   // timing experiments only (tools/build_unit_variant.sh)
+#define MG_EXP_COOP_ITERS 10
+#endif
 #ifndef MG_EXP_COOP_NORR   // timing experiments only: the lane-select robot rows below
     const int rb0 = ufirst(S.robot_body0[e]), rc0 = ufirst(S.robot_cons0[e]);
     if (robot_rows_static(S, e, G, unc, rb0, rc0)) {
@@ -1385,13 +1388,19 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
         rrows_cached(V, S, e, rc0, dt_coef);
         MG_PP(P, 5);
 #pragma unroll 1
-        for (int it = 0; it < 10; it++) {
+        for (int it = 0; it < MG_EXP_COOP_ITERS; it++) {
+#ifndef MG_EXP_COOP_NOARB
             for (int i = 0; i < unact; i++) xarb_apply(R, V, rb0, lane, S, e, ufirst(AT(S.active, i)));
+#endif
+#ifndef MG_EXP_COOP_NOGROUND
             if (G.n > 0) {
                 lground_apply(R, S, e, G.c0, dt);
                 if (G.n > 1) lground_apply(R, S, e, G.c1, dt);
             }
+#endif
+#ifndef MG_EXP_COOP_NOCONS
             rrows_apply(V, S, e, rc0, dt);
+#endif
         }
         // robot lanes: velocities from V (their bias velocities stayed in the lanes)
         if (lane < nb) {
@@ -1425,9 +1434,6 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
         lcons_cached(R, lane, S, e, c, ufirst(AT(S.ca, c)), cb, ufirst(AT(S.ctype, c)), dt_coef);
     }
     MG_PP(P, 5);
-#ifndef MG_EXP_COOP_ITERS   // timing experiments only (tools/build_unit_variant.sh)
-#define MG_EXP_COOP_ITERS 10
-#endif
 #pragma unroll 1
     for (int it = 0; it < MG_EXP_COOP_ITERS; it++) {
 #ifndef MG_EXP_COOP_NOARB

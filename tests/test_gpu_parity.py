@@ -141,7 +141,9 @@ KERNEL_FORMS = [
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,n,steps,env", KERNEL_FORMS)
+@pytest.mark.parametrize("name,n,steps,env", KERNEL_FORMS,
+                         ids=[f[0].split("-")[0] + "-" + "-".join(f"{k}{v}" for k, v in f[3].items())
+                              for f in KERNEL_FORMS])
 def test_step_kernel_forms(name, n, steps, env, monkeypatch):
     """Every step-kernel form gives the oracle's trajectories (a spread of envs across workgroups)."""
     for k, v in env.items():
