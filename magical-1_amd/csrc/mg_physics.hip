@@ -4,6 +4,8 @@
 #include "mg_launch.h"
 #include "mg_phys.h"   // sizeof(ShapeW) of the LDS views
 
+hipError_t mg_prof_read_step_quad(unsigned long long *out64);   // mg_step_quad.hip
+
 // LDS bytes of one env's view (same carve order as carve_view, per-lane columns)
 size_t mg_step_lds_bytes(const StepCaps &c, int blk) {
     size_t off = 0;
@@ -43,6 +45,7 @@ bool mg_step_blk_ok(int variant, int blk) {
     return variant == 0 ? (blk == 1 || blk == 8 || blk == 64)
          : variant == 3 ? (blk == 1 || blk == 4)
          : variant == 4 ? blk == 1
+         : variant == 5 || variant == 6 ? blk == 16
          : (blk == 1 || blk == 4 || blk == 16);
 }
 
@@ -55,6 +58,7 @@ hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, in
     MG_STEP_CASE(1, 1) MG_STEP_CASE(1, 4) MG_STEP_CASE(1, 16)
     MG_STEP_CASE(2, 1) MG_STEP_CASE(2, 4) MG_STEP_CASE(2, 16)
     MG_STEP_CASE(3, 1) MG_STEP_CASE(3, 4) MG_STEP_CASE(4, 1)
+    MG_STEP_CASE(5, 16) MG_STEP_CASE(6, 16)
     MG_STEP_CASE(0, 1) MG_STEP_CASE(0, 8) MG_STEP_CASE(0, 64)
 #undef MG_STEP_CASE
     return hipErrorInvalidValue;
@@ -66,5 +70,6 @@ hipError_t mg_prof_read_physics(unsigned long long *out) {
     if ((e = mg_prof_read_step_robot(out)) != hipSuccess) return e;
     if ((e = mg_prof_read_step_v3(out)) != hipSuccess) return e;
     if ((e = mg_prof_read_step_v4(out)) != hipSuccess) return e;
+    if ((e = mg_prof_read_step_quad(out)) != hipSuccess) return e;
     return mg_prof_read_step_hbm(out);
 }

@@ -182,8 +182,9 @@ static StepCaps step_caps(int task, int flags, int n_envs, const mg_library &lib
 }
 
 // Step kernel per scene (measured on MI355X, 8192 envs, ms per env-step of physics):
-// * compiled constraint lists (robot only / robot + one block): LDS variants 1/2, 16 envs per workgroup,
-//   one env per lane;
+// * compiled constraint lists (robot only / robot + one block): forms 5/6, 16 envs per 64-lane workgroup,
+//   4 lanes per env (4096 envs: MoveToRegion 0.62 ms, MoveToCorner 1.15; one env per lane, variants 1/2:
+//   0.73 / 1.42);
 // * every other scene (up to 8 blocks, runtime constraint lists): the cooperative LDS variant 4, one env
 //   per 64-lane wavefront with the order-free parts across lanes -- MatchRegions-TestAll 6.0 ms (variant
 //   3, one env per single-lane workgroup: 10.6; HBM-state kernel, 64 envs per wavefront: 21.1),
@@ -192,16 +193,18 @@ static int pick_step_variant(const StepCaps &c, int n_envs, int task) {
     (void)task;
     int v = mg_step_variant(c, n_envs);
     if (v == 3) v = 4;
+    if (v == 1 || v == 2) v += 4;
     const char *ov = getenv("MG_STEP_VARIANT");
-    if (ov) { // experiments: 0 (HBM state), the scene's compiled variant, 3 / 4 (LDS runtime lists)
+    if (ov) { // experiments: 0 (HBM state), the scene's compiled variant (1 / 2, or 5 / 6), 3 / 4 (LDS runtime lists)
         const int w = atoi(ov), base = mg_step_variant(c, n_envs);
         if (w == 0 || w == base || w == 3 || w == 4) v = w;   // 3 / 4 fit every scene (caps 14/53/26/48)
+        if ((base == 1 || base == 2) && w == base + 4) v = w;  // 5 / 6: the compiled lists, 4 lanes per env
     }
     return v;
 }
 
 static int pick_step_blk(int variant) {
-    int b = variant == 0 ? 64 : variant >= 3 ? 1 : 16;
+    int b = variant == 0 ? 64 : variant == 3 || variant == 4 ? 1 : 16;
     const char *ov = getenv(variant == 0 ? "MG_STEP_BLK0" : "MG_STEP_BLK"); // experiments
     if (ov && mg_step_blk_ok(variant, atoi(ov))) b = atoi(ov);
     return b;

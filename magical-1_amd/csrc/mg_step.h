@@ -243,8 +243,9 @@ MG_DEV void static_apply(const MGState &S, int e, double dt) {
 }
 
 // ---- arbiters ------------------------------------------------------------
-MG_DEV void arbiter_update(const MGState &S, const mg_library *L, int e, int key, const ShapeW &A, const ShapeW &B,
-                           double ua, double ub, const Collision &info) {
+// (ta, ba) / (tb, bb): world-shape type and body of the pair's shapes A / B in broadphase order
+MG_DEV void arbiter_update_t(const MGState &S, const mg_library *L, int e, int key, int ta, int ba, int tb, int bb,
+                             double ua, double ub, const Collision &info) {
     int na = S.arb_cap, slot = -1, free_slot = -1;
     for (int i = 0; i < na; i++) {
         int k = AT(S.akey, i);
@@ -257,10 +258,10 @@ MG_DEV void arbiter_update(const MGState &S, const mg_library *L, int e, int key
         AT(S.akey, slot) = key; AT(S.astate, slot) = ARB_FIRST; AT(S.acount, slot) = 0; AT(S.astamp, slot) = 0;
     }
     // info is in collision order: swapped => (a, b) = (B, A)
-    const ShapeW &sa = info.count >= 0 && A.type > B.type ? B : A;
-    const ShapeW &sb = A.type > B.type ? A : B;
-    double u_a = A.type > B.type ? ub : ua, u_b = A.type > B.type ? ua : ub;
-    V2 pa = bp(S, e, sa.body), pb = bp(S, e, sb.body);
+    const bool sw = ta > tb;
+    const int sa_body = sw ? bb : ba, sb_body = sw ? ba : bb;
+    double u_a = sw ? ub : ua, u_b = sw ? ua : ub;
+    V2 pa = bp(S, e, sa_body), pb = bp(S, e, sb_body);
     int oldc = AT(S.acount, slot);
     uint64_t oh0 = AHASH(0, slot), oh1 = AHASH(1, slot);
     double ojn0 = ACON(0, AC_JN, slot), ojt0 = ACON(0, AC_JT, slot);
@@ -279,12 +280,17 @@ MG_DEV void arbiter_update(const MGState &S, const mg_library *L, int e, int key
     AT(S.acount, slot) = info.count;
     AT(S.anx, slot) = info.n.x; AT(S.any, slot) = info.n.y;
     AT(S.au, slot) = u_a * u_b;
-    AT(S.asa, slot) = sa.body; AT(S.asb, slot) = sb.body;
+    AT(S.asa, slot) = sa_body; AT(S.asb, slot) = sb_body;
     if (AT(S.astate, slot) == ARB_CACHED) AT(S.astate, slot) = ARB_FIRST;
     int na_ = S.nactive[e];
     if (na_ < S.arb_cap) { AT(S.active, na_) = slot; S.nactive[e] = na_ + 1; }
     else S.overflow[e] |= 1;
     AT(S.astamp, slot) = S.stamp[e];
+}
+
+MG_DEV void arbiter_update(const MGState &S, const mg_library *L, int e, int key, const ShapeW &A, const ShapeW &B,
+                           double ua, double ub, const Collision &info) {
+    arbiter_update_t(S, L, e, key, A.type, A.body, B.type, B.body, ua, ub, info);
 }
 
 MG_DEV void arbiter_prestep(const MGState &S, const mg_library *L, int e, int slot, double dt) {

@@ -3,9 +3,18 @@
 // (mg_step_robot.hip, mg_step_v3.hip, mg_step_v4.hip, mg_step_hbm.hip) so they compile in parallel;
 // mg_physics.hip dispatches.
 #pragma once
+#include <cstdio>
 #include "mg_launch.h"
 #include "mg_step.h"
+#include "mg_stepq.h"
 #include "mg_score.h"
+
+// slot caps of every compiled form: the LDS variants of mg_launch.h, plus the QL-lanes-per-env forms of the
+// compile-time scenes (5: the caps of 1 with two world-shape slots per lane in LDS; 6: the caps of 2, world
+// shapes in per-lane locals as there)
+__host__ __device__ constexpr StepCaps step_form_caps(int v) {
+    return v == 5 ? StepCaps{6, 5, 10, 20, 16, 8} : v == 6 ? StepCaps{7, 6, 12, 32, 16, 0} : step_variant_caps(v);
+}
 
 // ---- LDS-resident substeps ------------------------------------------------
 // The 10 substeps of an env-step touch only the env's bodies, shapes,
@@ -163,38 +172,63 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
                                                   int auto_reset, const uint8_t *__restrict__ actions, float *reward,
                                                   uint8_t *done, double *eval_score, uint8_t *reset_mask) {
     extern __shared__ __align__(16) unsigned char smem[];
-    constexpr StepCaps C = step_variant_caps(VAR);
+    constexpr StepCaps C = step_form_caps(VAR);
     constexpr bool LDS = VAR != 0;
-    constexpr bool COOP = VAR == 4;          // one env per workgroup of 64 lanes
-    constexpr int NCS = VAR >= 3 ? 0 : C.nc; // compile-time constraint list (0: the env's runtime list)
-    const int lane = COOP ? (int)threadIdx.x : BLK == 1 ? 0 : (int)threadIdx.x;
-    const int e = xcd_block(blockIdx.x, gridDim.x) * BLK + (COOP ? 0 : lane);
-    if (e >= S.n_envs) return;
+    constexpr bool COOP = VAR == 4;            // one env per workgroup of 64 lanes
+    constexpr bool QUAD = VAR == 5 || VAR == 6; // QL lanes per env, BLK envs in one 64-lane workgroup
+    constexpr int QL = QUAD ? 64 / BLK : 1;
+    constexpr int NCS = VAR == 3 || VAR == 4 ? 0 : C.nc; // compile-time constraint list (0: the env's runtime list)
+    const int lane = COOP ? (int)threadIdx.x : QUAD ? (int)threadIdx.x / QL : BLK == 1 ? 0 : (int)threadIdx.x;
+    const int sub = QUAD ? (int)threadIdx.x % QL : 0;
+    int e = xcd_block(blockIdx.x, gridDim.x) * BLK + (COOP ? 0 : lane);
+    // QUAD: lanes without an env of their own (past n_envs, or a scene the form cannot hold) still take
+    // part in the workgroup barriers as shadows of a valid env; they never write HBM
+    bool shadow = false;
+    if (e >= S.n_envs) {
+        if (!QUAD) return;
+        shadow = true;
+        e = S.n_envs - 1;
+    }
     const int a = actions[e];
     MGProf P;
     MG_PP_INIT(P);
     if constexpr (LDS) {
+        bool fits = true;
         if (S.nbodies[e] > C.nb || S.nshapes[e] > C.ns || S.ncons[e] > C.nc) {
-            S.overflow[e] |= 16; // scene larger than the variant's LDS caps (never expected)
-            if (reset_mask) reset_mask[e] = 0;
-            return;
+            if (!shadow && sub == 0) {
+                S.overflow[e] |= 16; // scene larger than the variant's LDS caps (never expected)
+                if (reset_mask) reset_mask[e] = 0;
+            }
+            if (!QUAD) return;
+            fits = false;
         }
         bool ok = NCS == 0 || (S.ncons[e] == C.nc && S.robot_body0[e] == 0 && S.robot_cons0[e] == 0);
         for (int c = 0; c < NCS; c++) {
             const ConsDesc d = static_cons(c);
             ok = ok && AT(S.ctype, c) == d.type && AT(S.ca, c) == d.a && AT(S.cb, c) == d.b;
         }
-        for (int k = 0; k < S.nshapes[e] && NCS > 0; k++) ok = ok && shape_body_slot(AT(S.sbody, k)); // arb_body
-        if (!ok) { // the compiled constraint list does not describe this scene (never expected)
-            S.overflow[e] |= 32;
-            if (reset_mask) reset_mask[e] = 0;
-            return;
+        for (int k = 0; k < S.nshapes[e] && k < C.ns && NCS > 0; k++) ok = ok && shape_body_slot(AT(S.sbody, k)); // arb_body
+        if (!ok && fits) { // the compiled constraint list does not describe this scene (never expected)
+            if (!shadow && sub == 0) {
+                S.overflow[e] |= 32;
+                if (reset_mask) reset_mask[e] = 0;
+            }
+            if (!QUAD) return;
         }
         // the view is built from the LDS carve only (never merged with the HBM pointers), so every
         // access through it compiles to ds_* with a constant offset from the lane's column
         MGState V = S;
         carve_view(V, smem, C, BLK);
-        if constexpr (COOP) {
+        if constexpr (QUAD) {
+            const bool own = !shadow && fits && ok;
+            xfer_state(S, V, C, lane, e, true, false, sub, QL);
+            if (!fits && sub == 0) { // an empty scene in the env's column: nothing indexes past the caps
+                V.nbodies[lane] = 0; V.nshapes[lane] = 0; V.ncons[lane] = 0; V.nactive[lane] = 0;
+            }
+            env_substeps_quad<NCS, QL, (C.shw > 0)>(V, L, lane, sub, a, P);
+            if (own) xfer_state(S, V, C, lane, e, false, false, sub, QL);
+            if (!own || sub != 0) return;
+        } else if constexpr (COOP) {
             xfer_state(S, V, C, 0, e, true, true, lane, 64);
             __syncthreads();
             env_substeps_coop(V, L, lane, a, P);
@@ -226,16 +260,23 @@ template <int VAR, int BLK>
 hipError_t launch_step_var(const MGState &S, const mg_library *L, TaskCfg cfg, int max_steps, int auto_reset,
                                   const uint8_t *actions, float *reward, uint8_t *done, double *eval_score,
                                   uint8_t *reset_mask, hipStream_t st) {
-    constexpr StepCaps C = step_variant_caps(VAR);
+    constexpr StepCaps C = step_form_caps(VAR);
     const size_t lds = VAR == 0 ? 0 : mg_step_lds_bytes(C, BLK);
     static bool attr_set = false;
     if (VAR != 0 && !attr_set) {
         hipError_t err = hipFuncSetAttribute((const void *)step_kernel<VAR, BLK>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (err != hipSuccess) return err;
+        if (err != hipSuccess) {
+            fprintf(stderr, "step form %d/%d: LDS attribute %zu B: %s\n", VAR, BLK, lds, hipGetErrorString(err));
+            return err;
+        }
         attr_set = true;
     }
-    hipLaunchKernelGGL((step_kernel<VAR, BLK>), dim3((S.n_envs + BLK - 1) / BLK), dim3(VAR == 4 ? 64 : BLK), lds, st, S, L, cfg,
+    hipLaunchKernelGGL((step_kernel<VAR, BLK>), dim3((S.n_envs + BLK - 1) / BLK), dim3(VAR == 4 || VAR == 5 || VAR == 6 ? 64 : BLK), lds, st, S, L, cfg,
                        max_steps, auto_reset, actions, reward, done, eval_score, reset_mask);
-    return hipGetLastError();
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess)
+        fprintf(stderr, "step form %d/%d: launch of %d workgroups, LDS %zu B: %s\n", VAR, BLK,
+                (S.n_envs + BLK - 1) / BLK, lds, hipGetErrorString(err));
+    return err;
 }

@@ -18,7 +18,7 @@ OUT = os.path.join(HERE, "libmagical_sim.so")
 PROF_OUT = os.path.join(HERE, "libmagical_sim_prof.so")  # -DMG_PROFILE phase timers (tools/gpu_phase.py)
 _COMMON = ["mg_common.h", "mg_math.h", "mg_state.h", "mg_launch.h", "mg_prof.h"]
 _PHYS = _COMMON + ["mg_phys.h", "mg_step.h"]
-_STEP = _PHYS + ["mg_reset.h", "mg_score.h", "mg_stepk.h"]
+_STEP = _PHYS + ["mg_reset.h", "mg_score.h", "mg_stepk.h", "mg_stepq.h"]
 UNITS = {  # translation unit -> headers it depends on (one unit per kernel family: they compile in parallel)
     "mg_sim.hip": _COMMON + ["mg_phys.h"],
     "mg_physics.hip": _COMMON + ["mg_phys.h"],
@@ -26,6 +26,7 @@ UNITS = {  # translation unit -> headers it depends on (one unit per kernel fami
     "mg_step_robot.hip": _STEP,
     "mg_step_v3.hip": _STEP,
     "mg_step_v4.hip": _STEP,
+    "mg_step_quad.hip": _STEP,
     "mg_step_hbm.hip": _STEP,
     "mg_raster.hip": _PHYS + ["mg_render.h"],
     "mg_replay.hip": ["mg_common.h"],
