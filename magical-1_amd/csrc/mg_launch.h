@@ -20,6 +20,8 @@ struct RenderOut {
     int retry_out;        // ... a pair this class cannot hold is marked for the next class (else an env error)
     int cls_level;        // ... position of this class in the chain
     int force_retry;      // tests: classes below this level mark every pair (1: skip the first, 2: the first two)
+    int scache_mode;      // tests / A-B (MG_DEBUG_SCACHE): 1 = no allocentric static layer, 2 = its copied blocks
+                          // poisoned (0x55) -- shows where the layer is used
 };
 
 hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream_t st);

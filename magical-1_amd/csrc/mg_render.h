@@ -19,6 +19,7 @@
 #include "mg_launch.h"
 #include "mg_step.h"
 #include "mg_prof.h"
+#include <type_traits>
 
 // capacity classes (template parameters of the LDS layout): geoms, vertices, dash lines, bin entries
 // (outline items + fill edges, binned per band), solid outline edges, entities, outline-mask type (one bit
@@ -53,6 +54,11 @@
 #ifndef RG_DASH_SPLIT
 #define RG_DASH_SPLIT 1                 // dashes of dashed edges split over the workgroup (0: per edge thread)
 #endif
+#ifndef RG_SCACHE
+#define RG_SCACHE 1                     // allocentric static layer (S.scache): see render_kernel, section 5
+#endif
+#define RG_DMARGIN 4                    // px a geom's pixels can reach beyond its vertex bounds (outline width
+                                        // offsets, float/int end points)
 #define RG_EMPTY 32767
 #define RG_OSH (RG_OFS ? 3 : 0)         // resolve/outline-layer ordinal values are ordinal << RG_OSH
 #define RG_LOROW (MG_LORES * 3)         // bytes of one 96-px RGB row
@@ -114,8 +120,14 @@ struct RenderSmem {
         struct {
             uint32_t band[RG_BAND][MG_RES / MPW]; // outline layer of the current band (entity bits per pixel)
             uint4 lo[RG_BANDLO16];          // current frame, 2 LoRes rows
-            int32_t lk[RG_MAXLONG][7];      // long segments of this band (LineK)
-            int32_t lkr[RG_MAXLONG][3];     // klo, khi, ordinal
+            union {
+                struct {
+                    int32_t lk[RG_MAXLONG][7];      // long segments of this band (LineK)
+                    int32_t lkr[RG_MAXLONG][3];     // klo, khi, ordinal
+                };
+                uint4 los[RG_BANDLO16];     // the band's static-layer rows (episode's first allo frame; written
+                                            // after the long segments are drawn, read in the band's tail)
+            };
         } post;
     } u;
     uint2 ginfo[RG_MAXG];                     // (ymin | ymax << 16, xmin | xmax << 16), int16 halves
@@ -137,6 +149,9 @@ struct RenderSmem {
     uint16_t bin[RG_MAXBIN];                  // outline item index, or fill edge: vertex | closing << 14 | last-row << 15
     int16_t gslot[RG_MAXG];                   // band-list slot of each geom overlapping the current band
     int32_t ngeom, nsedge, ndash, nlong, nblist, err;
+    uint32_t smask;                           // entities without a body (arena, goals): the static layer
+    uint32_t dmask[2][3];                     // LoRes columns of a band that a body's geometry can reach (by band parity)
+    int32_t brng[2];                          // bands [brng[0], brng[1]) the band loop runs over
 #ifdef MG_PROFILE
     unsigned int pw[4];
 #endif
@@ -456,9 +471,10 @@ MG_DEV int xf_slot(int ent, int x) { return x == MG_XF_MAIN ? ent : SM::RG_MAXE 
 #define RG_SMALL_WPE 7                  // waves per SIMD the small class is compiled for: 72 VGPRs, 9 workgroups/CU
                                         // (measured: 7 -> 2.5% faster than the default 6; 8 = 64 VGPRs slower)
 #endif
+// medium-1 is compiled for 6 waves per SIMD (<= 80 VGPRs): its LDS allows 7 workgroups (21 waves) per CU
 template <class SM, int MODE>
 __global__ void __launch_bounds__(RG_THREADS)
-__attribute__((amdgpu_waves_per_eu((SM::RG_MAXG <= 32 && RG_SMALL_WPE) ? RG_SMALL_WPE : 1)))
+__attribute__((amdgpu_waves_per_eu((SM::RG_MAXG <= 32 && RG_SMALL_WPE) ? RG_SMALL_WPE : SM::RG_MAXG <= 48 ? 6 : 1)))
 render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     __shared__ SM sm;
     constexpr int mode = MODE;
@@ -491,6 +507,11 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     }
     if (tid < RG_NBANDS) { sm.u.pre.bin_cnt[tid] = 0; sm.u.pre.ebin_cnt[tid] = 0; }
     if (tid < 17) sm.oord1[tid] = 0;
+    if (tid < 64) {   // entities without a body (arena, goals): the static layer
+        const int k = tid < nents ? AT(S.ekind, tid) : MG_ENT_ROBOT;
+        const uint64_t b = __ballot(k == MG_ENT_ARENA || k == MG_ENT_GOAL);
+        if (tid == 0) sm.smask = (uint32_t)b;
+    }
 #if !RG_XF_LATE
     if (view == 0 && tid == 32) { // Viewer.render: stack.push(self.transform) -> eye(3) @ view
         const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
@@ -779,6 +800,18 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     const bool plain = fo || pp != MG_PREPROC_LORESSTACK;   // the view's own current-frame output
     // frame ring kept only where a stack reads it (LoRes3EA: ego ring, read by compose3ea_kernel)
     const bool keep_ring = stacked || (!fo && pp == MG_PREPROC_LORES3EA && view == 1);
+    // Allocentric static layer.  The body-less entities (arena, goals) and the allo view matrix are fixed
+    // for the whole episode, so the episode's first allo frame also resolves every block with those
+    // entities alone (entity-bit classes: the outline layer tells the entities apart) and writes that frame
+    // to S.scache; every later allo frame copies it into each 4x4 block that no geom of a body can reach
+    // (its vertex bounds + RG_DMARGIN) and resolves only the others -- bands that no body reaches skip the
+    // fill edges, outline lines and resolve altogether.  A block outside every body geom's reach has the
+    // same pixels in the full scene as in the static-only scene, so the frame is bit-identical.
+    const bool cview = RG_SCACHE && mode == 0 && view == 0 && out.scache_mode != 1;
+    const bool mk_cache = cview && fresh && !SM::ORDMAX;
+    const bool use_cache = cview && !fresh && S.scache_ok[e] != 0;
+    uint8_t *const scache = S.scache + (size_t)e * FR;
+    uint4 cpf = make_uint4(0, 0, 0, 0);   // wave 2, lanes 0-35: the next band's static-layer rows
     uint8_t *o_plain = view == 0 ? out.obs_allo : out.obs_ego;
     uint8_t *o_stack = pp == MG_PREPROC_LORESSTACK ? o_plain : out.obs_past;
     // 4x4 block of this thread: wave w covers block columns [32w, 32w + 32) of both block rows, so a
@@ -806,6 +839,8 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     // geoms whose rows meet band y0, in draw order (ballot compaction by one wave)
     auto band_list = [&](int y0) {
         int cnt = 0;
+        uint32_t *dm = sm.dmask[(y0 / RG_BAND) & 1];
+        if (use_cache && lane < 3) dm[lane] = 0u;   // same wave: ordered before the atomics below
         for (int base = 0; base < G; base += 64) {
             const int g = base + lane;
             bool ov = false;
@@ -814,6 +849,17 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                 const int ymin = (int16_t)(gi.x & 0xFFFF), ymax = (int16_t)(gi.x >> 16);
                 const int xmin = (int16_t)(gi.y & 0xFFFF), xmax = (int16_t)(gi.y >> 16);
                 ov = ymax >= y0 && ymin < y0 + RG_BAND && xmin <= xmax;
+                // LoRes columns of this band that a body geom can reach
+                if (use_cache && !((sm.smask >> sm.g_ent[g]) & 1u) && ymax + RG_DMARGIN >= y0 &&
+                    ymin - RG_DMARGIN < y0 + RG_BAND) {
+                    const int c0 = (xmin - RG_DMARGIN > 0 ? xmin - RG_DMARGIN : 0) >> 2;
+                    const int c1 = (xmax + RG_DMARGIN < MG_RES - 1 ? xmax + RG_DMARGIN : MG_RES - 1) >> 2;
+#pragma unroll
+                    for (int w = 0; w < 3; w++) {
+                        const int lo = c0 > 32 * w ? c0 : 32 * w, hi = c1 < 32 * w + 31 ? c1 : 32 * w + 31;
+                        if (lo <= hi) atomicOr(&dm[w], (hi - lo == 31 ? 0xFFFFFFFFu : ((1u << (hi - lo + 1)) - 1u)) << (lo - 32 * w));
+                    }
+                }
             }
             const uint64_t m = __ballot(ov);
             if (ov) {
@@ -826,6 +872,31 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         }
         if (lane == 0) sm.nblist = cnt;
     };
+    // Allocentric frame whose only output is its plain current frame (LoRes4E, LoRes3EA, frames-only): the
+    // bands outside the rows a body geom can reach are the static layer's rows, copied in bulk; the band
+    // loop runs over [band0, band1) only.  Elsewhere (frame rings / stacks to write) it runs over every band.
+    const bool brange = use_cache && !keep_ring && !stacked && plain;
+    auto body_rows = [&](int &b0, int &b1) {   // wave 2: the bands a body geom can reach
+        int y0 = MG_RES, y1 = -1;
+        for (int g = lane; g < G; g += 64) {
+            if ((sm.smask >> sm.g_ent[g]) & 1u) continue;
+            const uint2 gi = sm.ginfo[g];
+            const int ymin = (int16_t)(gi.x & 0xFFFF) - RG_DMARGIN, ymax = (int16_t)(gi.x >> 16) + RG_DMARGIN;
+            y0 = ymin < y0 ? ymin : y0; y1 = ymax > y1 ? ymax : y1;
+        }
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int a = __shfl_xor(y0, off), b = __shfl_xor(y1, off);
+            y0 = a < y0 ? a : y0; y1 = b > y1 ? b : y1;
+        }
+        y0 = y0 > 0 ? y0 : 0; y1 = y1 < MG_RES - 1 ? y1 : MG_RES - 1;
+        b0 = y0 <= y1 ? y0 / RG_BAND : 0;
+        b1 = y0 <= y1 ? y1 / RG_BAND + 1 : 0;
+    };
+    auto cache_prefetch = [&](int y0) {
+        if (use_cache && tid >= 128 && tid < 128 + RG_BANDLO16)
+            cpf = *(const uint4 *)(scache + (size_t)(y0 / 4) * RG_LOROW + 16 * (tid - 128));
+    };
     // band 0 prologue: outline layer cleared (it overlays the setup scratch: after the binning's
     // counters are done with), band list, prefetch (later bands: in the previous band's tail)
     if (do_pf) prefetch(0);
@@ -833,22 +904,55 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     for (int i = tid; i < (int)(sizeof(sm.u.post.band) / 16); i += RG_THREADS)
         ((uint4 *)&sm.u.post.band[0][0])[i] = make_uint4(0, 0, 0, 0);
     if (tid == 0) sm.nlong = 0;
-    if (tid >= 128) band_list(0);
+    if (tid >= 128) {
+        int b0 = 0, b1 = RG_NBANDS;
+        if (brange) body_rows(b0, b1);
+        if (lane == 0) { sm.brng[0] = b0; sm.brng[1] = b1; }
+        if (b0 < b1) band_list(RG_BAND * b0);
+        if (b0 < b1) cache_prefetch(RG_BAND * b0);
+    }
 #ifdef MG_PROFILE
     if (tid < 4) sm.pw[tid] = 0u;
 #endif
     RG_SYNC();
-    for (int y0 = 0, band_i = 0; y0 < MG_RES; y0 += RG_BAND, band_i++) {
+    const int band0 = __builtin_amdgcn_readfirstlane(sm.brng[0]), band1 = __builtin_amdgcn_readfirstlane(sm.brng[1]);
+    if (brange) {   // the static layer's rows outside [band0, band1): 36 x 16 B per band, 2 per thread per round
+        const int nst = (RG_NBANDS - (band1 - band0)) * RG_BANDLO16;
+        for (int i0 = tid; i0 < nst; i0 += 2 * RG_THREADS) {
+            uint4 v[2];
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int i = i0 + k * RG_THREADS;
+                const int b = i / RG_BANDLO16, bb = b < band0 ? b : b + (band1 - band0);
+                const size_t o = (size_t)bb * RG_BANDLO + 16 * (i % RG_BANDLO16);
+                v[k] = i < nst ? *(const uint4 *)(scache + o) : make_uint4(0, 0, 0, 0);
+                if (out.scache_mode == 2) v[k] = make_uint4(0x55555555u, 0x55555555u, 0x55555555u, 0x55555555u);
+            }
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int i = i0 + k * RG_THREADS;
+                const int b = i / RG_BANDLO16, bb = b < band0 ? b : b + (band1 - band0);
+                if (i < nst) *(uint4 *)(o_plain + (size_t)e * FR + (size_t)bb * RG_BANDLO + 16 * (i % RG_BANDLO16)) = v[k];
+            }
+        }
+    }
+    for (int y0 = RG_BAND * band0, band_i = band0; band_i < band1; y0 += RG_BAND, band_i++) {
         const size_t lrow = (size_t)(y0 / 4) * RG_LOROW;  // byte offset of this band's LoRes rows
         MG_PROF(1);
         MG_PROF_MARK(t_lines);
         // fill spans of this band's rows: each binned fill edge writes its chain's intersection
         // (side 0: edges going down the vertex order, side 1: going up) of the rows it meets here
         const int nbl = sm.nblist;
+        // static layer: this band's rows first (blocks that need a resolve overwrite theirs after the
+        // barrier below); a band that no body geom reaches is the static layer's rows
+        const uint32_t *dmb = sm.dmask[band_i & 1];
+        const bool sband = use_cache && __builtin_amdgcn_readfirstlane(dmb[0] | dmb[1] | dmb[2]) == 0u;
+        if (use_cache && tid >= 128 && tid < 128 + RG_BANDLO16)
+            sm.u.post.lo[tid - 128] = out.scache_mode == 2 ? make_uint4(0x55555555u, 0x55555555u, 0x55555555u, 0x55555555u) : cpf;
         // (wave 1; the outline items run on waves 0 and 2 at the same time)
         const bool fwave = tid >= 64 && tid < 128;
         const int lt = tid < 64 ? tid : tid - 64;   // outline-item thread index (waves 0, 2)
-        for (int j = sm.ebin_off[band_i] + nout + tid - 64; fwave && j < sm.ebin_off[band_i + 1] + nout && !(dskip & 8); j += 64) {
+        for (int j = sm.ebin_off[band_i] + nout + tid - 64; fwave && !sband && j < sm.ebin_off[band_i + 1] + nout && !(dskip & 8); j += 64) {
             // fill_edge without the geom-bounds lookup: the bin entry carries the closing and last-row flags
             const int ve = sm.bin[j];
             const int v = ve & 0x3FFF, g = sm.v_geom[v];
@@ -877,7 +981,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                 if (r >= d) { r -= d; q++; }
             }
         }
-        if (RG_SPANW && fwave) {
+        if (RG_SPANW && fwave && !sband) {
             // each row's two chain intersections -> (l, w = r - l); a row missing either intersection is
             // empty: l = RG_EMPTY, w = 0 (no pixel has x = 32767).  Only this wave writes bspan in the band.
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's span writes are done
@@ -892,7 +996,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         // outline items of this band: solid width-2 edges (clip_and_draw_line_width: base line plus one
         // offset copy, each clipped) and clipped dashed-goal lines
         // (one thread per segment: solid edges contribute two, dash lines one)
-        for (int j2 = 2 * sm.bin_off[band_i] + lt / RG_SEGLANES; !fwave && j2 < 2 * sm.bin_off[band_i + 1] && !(dskip & 1);
+        for (int j2 = 2 * sm.bin_off[band_i] + lt / RG_SEGLANES; !fwave && !sband && j2 < 2 * sm.bin_off[band_i + 1] && !(dskip & 1);
              j2 += 128 / RG_SEGLANES) {
             const int i = sm.bin[j2 >> 1], c = j2 & 1;
             int x1, y1, x2, y2;
@@ -915,7 +1019,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
             segment_band(sm, x1, y1, x2, y2, ord, y0, lt % RG_SEGLANES);
         }
         MG_PROF_MAXW(sm.pw[0], t_lines);
-        RG_SYNC();
+        if (!sband) RG_SYNC();   // sband is uniform (LDS read after a barrier)
         const int nlong = sm.nlong;
         if (nlong > 0) {
             for (int q = 0; q < nlong && q < RG_MAXLONG; q++) {
@@ -934,7 +1038,11 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         // fill wins), max with the outline layer, colour, then the area sum of the block
         uint8_t *lo8 = (uint8_t *)sm.u.post.lo;
         MG_PROF_MARK(t_fill);
-        {
+        const bool need = !use_cache || ((dmb[ox >> 5] >> (ox & 31)) & 1u);
+        // pass 0: the frame (skipped where the static layer stands); pass 1 (the episode's first allo frame):
+        // the static layer, the body-less entities alone
+        auto resolve = [&](auto sonly_c) {
+            constexpr bool sonly = decltype(sonly_c)::value;
             const int yb = 4 * oyl, ya = y0 + yb;
             uint32_t o[4][4];
 #pragma unroll
@@ -948,6 +1056,8 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                 const uint32_t xr = sm.bxr[slot];
                 const int xmin = (int16_t)(xr & 0xFFFF), xmax = (int16_t)(xr >> 16);
                 if (xmax < x0 || xmin > x0 + 3) continue;
+                if constexpr (sonly)
+                    if (!((sm.smask >> sm.g_ent[sm.blist[slot]]) & 1u)) continue;
                 const uint4 s4 = *(const uint4 *)&sm.bspan[slot][yb];
                 const uint32_t ord = (2 * (uint32_t)sm.blist[slot] + 1) << RG_OSH;
 #pragma unroll
@@ -988,7 +1098,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
 #pragma unroll
                         for (int c = 0; c < 4; c++) {
                             const uint32_t wc = (SM::MPW == 4 || c < 2) ? w0 : w1;
-                            const uint32_t m = (wc >> (SM::MBITS * (c % SM::MPW))) & SM::MMASK;
+                            const uint32_t m = (wc >> (SM::MBITS * (c % SM::MPW))) & (sonly ? sm.smask : SM::MMASK);
                             const uint32_t oo = sm.oord1[m ? 32 - __clz((int)m) : 0];
                             o[r][c] = o[r][c] > oo ? o[r][c] : oo;
                         }
@@ -1011,14 +1121,17 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                     }
                 }
             } else {
+                uint8_t *dst8 = sonly ? (uint8_t *)sm.u.post.los : lo8;
                 for (int ch = 0; ch < ((dskip & 256) ? 0 : 3); ch++) {
                     const int ss = (int)((sum >> (16 * ch)) & 0xFFFF);
                     // round half to even of ss / 16: + 7, + 1 more when ss / 16 is odd
-                    if (RG_OFS) lo8[lpix * 3 + ch] = (uint8_t)((ss + 7 + ((ss >> 4) & 1)) >> 4);
-                    else { const int q = ss >> 4, rm = ss & 15; lo8[lpix * 3 + ch] = (uint8_t)(q + (rm > 8 || (rm == 8 && (q & 1)))); }
+                    if (RG_OFS) dst8[lpix * 3 + ch] = (uint8_t)((ss + 7 + ((ss >> 4) & 1)) >> 4);
+                    else { const int q = ss >> 4, rm = ss & 15; dst8[lpix * 3 + ch] = (uint8_t)(q + (rm > 8 || (rm == 8 && (q & 1)))); }
                 }
             }
-        }
+        };
+        if (need) resolve(std::false_type{});
+        if (mk_cache) resolve(std::true_type{});
         MG_PROF_MAXW(sm.pw[1], t_fill);
         RG_SYNC();
         MG_PROF(3);
@@ -1038,13 +1151,17 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
             if (tid >= 64) {
                 // ring of the last 4 LoRes frames: slot nh (all 4 slots at episode start)
                 const int nring = keep_ring ? (fresh ? 4 : 1) * RG_BANDLO16 : 0;
-                for (int t = tid - 64; t < nring + (plain ? RG_BANDLO16 : 0); t += RG_THREADS - 64) {
+                const int nplain = nring + (plain ? RG_BANDLO16 : 0);
+                for (int t = tid - 64; t < nplain + (mk_cache ? RG_BANDLO16 : 0); t += RG_THREADS - 64) {
                     if (t < nring) {
                         const int sl = fresh ? t / RG_BANDLO16 : nh, c = t % RG_BANDLO16;
                         *(uint4 *)(ring + ((size_t)sl * S.N + e) * FR + lrow + 16 * c) = sm.u.post.lo[c];
-                    } else {
+                    } else if (t < nplain) {
                         const int c = t - nring;
                         *(uint4 *)(o_plain + (size_t)e * FR + lrow + 16 * c) = sm.u.post.lo[c];
+                    } else {
+                        const int c = t - nplain;
+                        *(uint4 *)(scache + lrow + 16 * c) = sm.u.post.los[c];
                     }
                 }
             } else if (stacked && tid < 2 * MG_LORES / 4 && !(dskip & 64)) {
@@ -1071,15 +1188,17 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                 dst[2] = make_uint4(o[8], o[9], o[10], o[11]);
             }
         }
-        if (y0 + RG_BAND < MG_RES) {
+        if (band_i + 1 < band1) {
             if (tid >= 128) band_list(y0 + RG_BAND);
             if (do_pf) prefetch(y0 + RG_BAND);
+            cache_prefetch(y0 + RG_BAND);
         }
         RG_SYNC();
         MG_PROF(4);
     }
     if (sm.err) { if (tid == 0) S.overflow[e] |= 4 << view; }
     if (mode == 0 && tid == 0) S.hist_head[view * S.N + e] = nh;
+    if (cview && fresh && tid == 0) S.scache_ok[e] = mk_cache ? 1 : 0;
     MG_PROF_END(16 * view);
 }
 #undef RG_FAIL

@@ -27,9 +27,27 @@ static int set_err(int code, const std::string &msg) {
         if (_e != hipSuccess) return set_err(-5, std::string(#x) + ": " + hipGetErrorString(_e));      \
     } while (0)
 
+// one [slot][N] row of the per-env state: env e's element is at pool + off + e * esize
+struct StateRow { uint64_t off; uint32_t esize, pad; };
+
 struct mg_sim {
     MGState S;
+    // Next-layout shadow (reset prefetch).  BaseEnv.reset draws the whole layout from the env's RNG and
+    // nothing else (mg_reset.h reset_env), so the layout of an env's NEXT episode is known as soon as its
+    // current one starts.  SH is a second copy of the per-env state (same layout, no frame rings): right
+    // after an env resets, reset_kernel runs on SH for it on a side stream, overlapping the step and render
+    // kernels; when the episode ends the auto-reset is a copy SH -> S of that env (reset_copy_kernel).
+    MGState SH;
+    void *shadow_pool;
+    StateRow *rows;        // device table of the per-env state rows (both pools)
+    int nrows;
+    uint8_t *pend;         // device u8[N]: envs whose shadow the side stream is preparing
+    hipStream_t side;
+    hipEvent_t ev_copied, ev_prepared;
+    int shadow_ok;         // every env's shadow holds its next layout (set by a full mg_reset)
+    int shadow_pending;    // a reset_kernel on SH is in flight on the side stream
     int force_render_retry;   // tests: the first k render classes of the chain hand every (env, view) on
+    int scache_mode;          // tests: RenderOut::scache_mode
     mg_library *dlib;
     void *pool;
     size_t pool_bytes;
@@ -101,21 +119,62 @@ __global__ void __launch_bounds__(256) actions_kernel(uint8_t *out, int n, uint6
     out[e] = (uint8_t)(c0 % 18u);
 }
 
+// env e's per-env state rows src -> dst for the envs in mask (pend[e] = mask[e] for every env): the
+// auto-reset from the next-layout shadow (src = shadow, to_main), or an explicit reset's state handed to
+// the shadow (src = main).  Error flags: bit 2 (PlacementError of this reset) and the sticky bit 64 come
+// from the reset that produced the layout.
+__global__ void __launch_bounds__(256) reset_copy_kernel(const char *__restrict__ src, char *__restrict__ dst,
+                                                         const StateRow *__restrict__ rows, int nrows,
+                                                         const uint8_t *__restrict__ mask, uint8_t *__restrict__ pend,
+                                                         MGState S, MGState SH, int to_main) {
+    const int e = blockIdx.x, tid = threadIdx.x;
+    if (e >= S.n_envs) return;
+    const bool m = mask ? mask[e] != 0 : true;
+    if (tid == 0) pend[e] = m ? 1 : 0;
+    if (!m) return;
+    for (int r = tid; r < nrows; r += 256) {
+        const StateRow w = rows[r];
+        const size_t o = w.off + (size_t)e * w.esize;
+        switch (w.esize) {
+        case 8: *(uint64_t *)(dst + o) = *(const uint64_t *)(src + o); break;
+        case 4: *(uint32_t *)(dst + o) = *(const uint32_t *)(src + o); break;
+        case 2: *(uint16_t *)(dst + o) = *(const uint16_t *)(src + o); break;
+        default: dst[o] = src[o]; break;
+        }
+    }
+    if (tid == 0) {
+        if (to_main) {
+            S.overflow[e] = (S.overflow[e] & ~2) | (SH.overflow[e] & (2 | 64));
+            if (S.target_out) {   // PickAndPlace: reset_env writes the bound target output at reset
+                double *t = S.target_out + 4 * (size_t)e;
+                t[0] = SH.tgt_ids[e]; t[1] = SH.tgt_ids[S.N + e]; t[2] = SH.tgt_x[e]; t[3] = SH.tgt_y[e];
+            }
+        } else {
+            SH.overflow[e] = S.overflow[e];
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // allocation
 struct Carver {
     char *base;
     size_t off;
+    std::vector<StateRow> *rows = nullptr;   // records every take as [n / N] rows (n = slots x N)
+    size_t N = 0;
     template <typename T> T *take(size_t n) {
         off = (off + 255) & ~(size_t)255;
         T *p = (T *)(base ? base + off : nullptr);
+        if (rows)
+            for (size_t k = 0; k < n / N; k++) rows->push_back(StateRow{off + k * N * sizeof(T), (uint32_t)sizeof(T), 0u});
         off += n * sizeof(T);
         return p;
     }
 };
 
-static void layout(MGState &S, Carver &c) {
+static void layout(MGState &S, Carver &c, bool frames = true) {
     size_t N = (size_t)S.N;
+    c.N = N;
     size_t B = MG_MAX_BODIES * N, SH = MG_MAX_SHAPES * N, C = MG_MAX_CONS * N, A = MG_MAX_ARB * N, E = MG_MAX_ENTS * N;
     S.bpx = c.take<double>(B); S.bpy = c.take<double>(B); S.bvx = c.take<double>(B); S.bvy = c.take<double>(B);
     S.ba = c.take<double>(B); S.bw = c.take<double>(B); S.bvbx = c.take<double>(B); S.bvby = c.take<double>(B);
@@ -135,8 +194,13 @@ static void layout(MGState &S, Carver &c) {
     S.anx = c.take<double>(A); S.any = c.take<double>(A); S.au = c.take<double>(A);
     S.acon = c.take<double>((size_t)2 * AC_NUM * A); S.ahash = c.take<uint64_t>(2 * A);
     S.active = c.take<int8_t>(A); S.nactive = c.take<int32_t>(N); S.stamp = c.take<uint32_t>(N);
-    S.curr_dt = c.take<double>(N); S.overflow = c.take<int32_t>(N);
-    S.rg_retry = c.take<uint8_t>(2 * N);
+    S.curr_dt = c.take<double>(N);
+    {   // not state rows: the error flags are merged by reset_copy_kernel, rg_retry is render scratch
+        std::vector<StateRow> *r = c.rows;
+        c.rows = nullptr;
+        S.overflow = c.take<int32_t>(N); S.rg_retry = c.take<uint8_t>(2 * N);
+        c.rows = r;
+    }
     S.target_speed = c.take<double>(N); S.rel_turn = c.take<double>(N); S.target_finger = c.take<double>(N);
     S.robot_body0 = c.take<int32_t>(N); S.robot_cons0 = c.take<int32_t>(N); S.pv = c.take<double>(5 * N);
     S.ekind = c.take<int8_t>(E); S.etype = c.take<int8_t>(E); S.ecol = c.take<int8_t>(E); S.erole = c.take<int8_t>(E);
@@ -148,9 +212,12 @@ static void layout(MGState &S, Carver &c) {
     S.tgt_x = c.take<double>(N); S.tgt_y = c.take<double>(N);
     S.target_out = nullptr;
     S.mt_key = c.take<uint32_t>(624 * N); S.mt_pos = c.take<int32_t>(N);
+    c.rows = nullptr;   // state rows end here (frames and render scratch below are not part of a layout)
+    if (!frames) { S.hist_allo = S.hist_ego = S.scache = S.scache_ok = nullptr; S.hist_head = nullptr; return; }
     size_t FR = (size_t)MG_LORES * MG_LORES * 3;
     S.hist_allo = c.take<uint8_t>(4 * N * FR); S.hist_ego = c.take<uint8_t>(4 * N * FR);
     S.hist_head = c.take<int32_t>(2 * N);
+    S.scache = c.take<uint8_t>(N * FR); S.scache_ok = c.take<uint8_t>(N);
 }
 
 static hipStream_t as_stream(void *s) { return (hipStream_t)s; }
@@ -219,6 +286,7 @@ static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
     ro.debug_skip = 0;
     ro.small = s->task == MG_TASK_MOVE_TO_REGION || s->task == MG_TASK_MOVE_TO_CORNER;
     ro.force_retry = s->force_render_retry;
+    ro.scache_mode = s->scache_mode;
 #ifdef MG_PROFILE
     if (getenv("MG_DEBUG_SKIP")) ro.debug_skip = atoi(getenv("MG_DEBUG_SKIP"));
 #endif
@@ -228,6 +296,24 @@ static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
     HIPC(mg_launch_render(s->S, s->dlib, ro, 0, st));
     if (s->preproc == MG_PREPROC_LORES3EA && !s->out.frames_only)
         HIPC(mg_launch_compose3ea(s->S, (const uint8_t *)s->out.obs_allo, mask, (uint8_t *)s->out.obs_past, st));
+    return 0;
+}
+
+// hand the state of the envs in mask (null: all) from one pool to the other on st, then prepare their
+// next layouts on the side stream (reset_kernel on the shadow)
+static int shadow_handover(mg_sim *s, hipStream_t st, const uint8_t *mask, int to_main) {
+    if (s->shadow_pending) HIPC(hipStreamWaitEvent(st, s->ev_prepared, 0));   // pend and the shadow are free
+    const char *src = (const char *)(to_main ? s->shadow_pool : s->pool);
+    char *dst = (char *)(to_main ? s->pool : s->shadow_pool);
+    hipLaunchKernelGGL(reset_copy_kernel, dim3(s->S.n_envs), dim3(256), 0, st, src, dst, s->rows, s->nrows, mask,
+                       s->pend, s->S, s->SH, to_main);
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(s->ev_copied, st));
+    HIPC(hipStreamWaitEvent(s->side, s->ev_copied, 0));
+    TaskCfg cfg = {s->task, s->flags};
+    HIPC(mg_launch_reset(s->SH, s->dlib, cfg, s->pend, s->side));
+    HIPC(hipEventRecord(s->ev_prepared, s->side));
+    s->shadow_pending = 1;
     return 0;
 }
 
@@ -271,8 +357,11 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     if (const char *mt = getenv("MG_DEBUG_MAX_TRIES")) s->S.max_tries = atoi(mt) > 0 ? atoi(mt) : 10000; // tests only
     if (const char *rr = getenv("MG_DEBUG_RENDER_RETRY")) s->force_render_retry = atoi(rr);                 // tests only
     else s->force_render_retry = 0;
+    s->scache_mode = getenv("MG_DEBUG_SCACHE") ? atoi(getenv("MG_DEBUG_SCACHE")) : 0;                    // tests only
     s->S.N = (cfg->num_envs + 63) / 64 * 64;
+    std::vector<StateRow> rows;
     Carver sizing = {nullptr, 0};
+    sizing.rows = &rows;
     layout(s->S, sizing);
     s->pool_bytes = sizing.off + 256;
     hipError_t err = hipMalloc(&s->pool, s->pool_bytes);
@@ -289,6 +378,30 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     err = hipMalloc((void **)&s->reset_mask, (size_t)s->S.N);
     if (err != hipSuccess) { (void)hipFree(s->pool); (void)hipFree(s->dlib); delete s; return set_err(-12, "mg_create: hipMalloc mask"); }
     HIPC(hipMemset(s->reset_mask, 0, (size_t)s->S.N));
+    // next-layout shadow: the many-block tasks, whose rejection-sampled layouts make a reset long (the
+    // robot scenes reset in ~0.03 ms); MG_RESET_PREFETCH=0/1 overrides
+    s->shadow_pool = nullptr; s->rows = nullptr; s->pend = nullptr; s->side = nullptr;
+    s->shadow_ok = 0; s->shadow_pending = 0; s->nrows = 0;
+    bool prefetch = s->auto_reset && s->task != MG_TASK_MOVE_TO_REGION && s->task != MG_TASK_MOVE_TO_CORNER;
+    if (const char *pf = getenv("MG_RESET_PREFETCH")) prefetch = s->auto_reset && atoi(pf) != 0;
+    if (prefetch) {
+        s->SH = s->S;
+        s->SH.target_out = nullptr;
+        Carver ssz = {nullptr, 0};
+        layout(s->SH, ssz, false);
+        HIPC(hipMalloc(&s->shadow_pool, ssz.off + 256));
+        HIPC(hipMemset(s->shadow_pool, 0, ssz.off + 256));
+        Carver sreal = {(char *)s->shadow_pool, 0};
+        layout(s->SH, sreal, false);
+        s->nrows = (int)rows.size();
+        HIPC(hipMalloc((void **)&s->rows, rows.size() * sizeof(StateRow)));
+        HIPC(hipMemcpy(s->rows, rows.data(), rows.size() * sizeof(StateRow), hipMemcpyHostToDevice));
+        HIPC(hipMalloc((void **)&s->pend, (size_t)s->S.N));
+        HIPC(hipMemset(s->pend, 0, (size_t)s->S.N));
+        HIPC(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+        HIPC(hipEventCreateWithFlags(&s->ev_copied, hipEventDisableTiming));
+        HIPC(hipEventCreateWithFlags(&s->ev_prepared, hipEventDisableTiming));
+    }
     std::vector<uint32_t> seeds(cfg->num_envs);
     for (int i = 0; i < cfg->num_envs; i++) seeds[i] = cfg->seeds ? cfg->seeds[i] : cfg->base_seed + (uint32_t)i;
     *out = s;
@@ -298,6 +411,9 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
 int mg_seed(mg_sim *s, const uint32_t *seeds_host) {
     if (!s || !seeds_host) return set_err(-22, "mg_seed: null argument");
     HIPC(hipSetDevice(s->device));
+    if (s->shadow_pending) HIPC(hipEventSynchronize(s->ev_prepared));
+    s->shadow_pending = 0;
+    s->shadow_ok = 0;   // the shadow's layouts came from the old seeds: valid again after a full mg_reset
     uint32_t *d = nullptr;
     HIPC(hipMalloc(&d, sizeof(uint32_t) * s->S.n_envs));
     HIPC(hipMemcpy(d, seeds_host, sizeof(uint32_t) * s->S.n_envs, hipMemcpyHostToDevice));
@@ -335,6 +451,11 @@ int mg_reset(mg_sim *s, const uint8_t *mask, void *stream) {
     hipStream_t st = as_stream(stream);
     TaskCfg cfg = {s->task, s->flags};
     HIPC(mg_launch_reset(s->S, s->dlib, cfg, mask, st));
+    if (s->shadow_pool) {
+        const int rc = shadow_handover(s, st, mask, 0);
+        if (rc) return rc;
+        if (!mask) s->shadow_ok = 1;
+    }
     if (s->preproc != MG_PREPROC_NONE) return render_lores(s, st, mask);
     return 0;
 }
@@ -351,7 +472,14 @@ int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
     HIPC(mg_launch_step(s->S, s->dlib, cfg, s->step_variant, s->step_blk, s->max_steps, s->auto_reset, actions, s->out.reward,
                         s->out.done, s->out.eval_score, s->reset_mask, st));
     if (ev) HIPC(hipEventRecord(ev[1], st));
-    if (s->auto_reset) HIPC(mg_launch_reset(s->S, s->dlib, cfg, s->reset_mask, st));
+    if (s->auto_reset) {
+        if (s->shadow_ok) {
+            const int rc = shadow_handover(s, st, s->reset_mask, 1);
+            if (rc) return rc;
+        } else {
+            HIPC(mg_launch_reset(s->S, s->dlib, cfg, s->reset_mask, st));
+        }
+    }
     if (ev) HIPC(hipEventRecord(ev[2], st));
     int rc = 0;
     if (s->preproc != MG_PREPROC_NONE) rc = render_lores(s, st, nullptr);
@@ -525,6 +653,12 @@ void mg_destroy(mg_sim *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
+    if (s->side) {
+        (void)hipStreamSynchronize(s->side);
+        (void)hipEventDestroy(s->ev_copied); (void)hipEventDestroy(s->ev_prepared);
+        (void)hipStreamDestroy(s->side);
+        (void)hipFree(s->shadow_pool); (void)hipFree(s->rows); (void)hipFree(s->pend);
+    }
     (void)hipFree(s->pool);
     (void)hipFree(s->dlib);
     (void)hipFree(s->reset_mask);

@@ -66,6 +66,11 @@ struct MGState {
     uint8_t *hist_allo;      // [4][N][96*96*3]
     uint8_t *hist_ego;       // [4][N][96*96*3]
     int32_t *hist_head;      // [N] ring head
+    // allocentric static layer: the LoRes allo frame of the env's body-less entities alone (arena, goals --
+    // fixed for the whole episode), written by the episode's first allo render; a 4x4 block that no
+    // body's geometry reaches copies it instead of being resolved (render_kernel)
+    uint8_t *scache;         // [N][96*96*3]
+    uint8_t *scache_ok;      // [N] 1: scache holds this episode's static layer
     // LDS views of the compile-time robot scenes: 3 world-space shapes per lane (narrowphase operands:
     // the queried shape, a wall, the other shape) in LDS instead of per-lane scratch; null elsewhere
     ShapeW *shw;

@@ -399,6 +399,113 @@ def test_full_size_sampled_parity(name, n, steps, L):
     vec.close()
 
 
+# Auto-reset paths (mg_sim.hip): the next-layout shadow (default for the many-block tasks: the next
+# episode's layout is sampled on a side stream while the current one runs, and the auto-reset copies it in)
+# and the in-place reset_kernel (default for the robot scenes), each forced both ways with short episodes,
+# plus a re-seed and a masked explicit reset while the shadow is live.
+RESET_PATHS = [
+    ("MatchRegions-TestAll-LoRes4E-v0", 66, 40, 7, {}),
+    ("MatchRegions-TestAll-LoRes4E-v0", 66, 40, 7, {"MG_RESET_PREFETCH": "0"}),
+    ("ClusterColour-TestAll-LoResStack-v0", 66, 30, 4, {}),
+    ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, 5, {"MG_RESET_PREFETCH": "1"}),
+    ("PickAndPlace-Demo-LoResCHW4A-v0", 8, 30, 4, {}),
+    ("FindDupe-TestAll-LoRes4E-v0", 66, 30, 1, {}),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n,steps,L,env", RESET_PATHS,
+                         ids=[f"{f[0].split('-')[0]}-L{f[3]}-" + "-".join(f"{k}{v}" for k, v in f[4].items())
+                              for f in RESET_PATHS])
+def test_reset_paths(name, n, steps, L, env, monkeypatch):
+    """Auto-resets every L steps through either reset path equal the oracle's resets (observations,
+    bodies, done / score, PickAndPlace targets, error flags); then the envs are re-seeded, run again, and
+    a masked explicit reset is issued mid-episode with auto-reset on."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    spec = registry.lookup(name)
+    pick = sorted(i for i in {0, 1, 17, 63, 64, n - 1} if i < n)
+
+    def run(seeds, acts, masked_at=None):
+        orc = {i: po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, L, seed=seeds[i]) for i in pick}
+        obs = vec.reset()
+        for i in pick:
+            ref = with_targets(spec, oracle_obs_split(spec, orc[i].reset()), orc[i])
+            for k in obs:
+                assert np.array_equal(obs[k][i].cpu().numpy(), ref[k]), f"reset env {i} {k}"
+        mask = np.zeros(n, dtype=np.uint8)
+        mask[pick[1::2]] = 1
+        for t in range(acts.shape[0]):
+            if t == masked_at:
+                obs = vec.reset(torch.as_tensor(mask))
+                for i in pick:
+                    if mask[i]:
+                        ref = with_targets(spec, oracle_obs_split(spec, orc[i].reset()), orc[i])
+                        for k in obs:
+                            assert np.array_equal(obs[k][i].cpu().numpy(), ref[k]), f"masked reset env {i} {k}"
+            obs, rew, done, info = vec.step(torch.as_tensor(acts[t], dtype=torch.uint8))
+            got = {k: v[pick].cpu().numpy() for k, v in obs.items()}
+            got_done = done[pick].cpu().numpy()
+            got_score = info["eval_score"][pick].cpu().numpy()
+            bodies = vec.bodies()[0][pick].cpu().numpy()
+            for j, i in enumerate(pick):
+                o, r, d, sc = orc[i].step(int(acts[t, i]))
+                assert bool(got_done[j]) == d and got_score[j] == sc, f"step {t} env {i}"
+                if d:
+                    o = orc[i].reset()
+                else:
+                    b = orc[i].bodies()
+                    assert np.abs(bodies[j, :len(b)] - b).max() <= POSE_TOL, f"step {t} env {i} bodies"
+                ref = with_targets(spec, oracle_obs_split(spec, o), orc[i])
+                for k in got:
+                    assert np.array_equal(got[k][j], ref[k]), f"step {t} env {i} obs {k}"
+
+    seeds = [700 + i for i in range(n)]
+    vec = magical_amd.make_vec(name, n, seeds=seeds, max_episode_steps=L)
+    run(seeds, np.random.RandomState(3).randint(0, 18, (steps, n)))
+    seeds2 = [9000 + 3 * i for i in range(n)]
+    vec.seed(seeds2)
+    run(seeds2, np.random.RandomState(4).randint(0, 18, (steps, n)), masked_at=steps // 2 + 1)
+    assert int(vec.errors().abs().sum().item()) == 0
+    vec.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n", [("MoveToRegion-Demo-LoRes4E-v0", 64), ("MatchRegions-TestAll-LoRes4E-v0", 64)])
+def test_allo_static_layer_in_use(name, n, monkeypatch):
+    """The allocentric static layer (render_kernel: arena + goals rendered once per episode, copied into
+    every 4x4 block no body geom reaches) is really used: with its copied blocks poisoned
+    (MG_DEBUG_SCACHE=2) the reset frames are still exact and later allo frames carry the poison outside
+    the bodies' reach, while the ego view is untouched; with the layer off (=1) every frame equals the
+    oracle.  (The default path's parity is every other rollout test.)"""
+    spec = registry.lookup(name)
+    seeds = [40 + i for i in range(n)]
+    acts = np.random.RandomState(8).randint(0, 18, (6, n))
+    for mode in ("2", "1"):
+        monkeypatch.setenv("MG_DEBUG_SCACHE", mode)
+        vec = magical_amd.make_vec(name, n, seeds=seeds)
+        orc = [oracle_env(spec, s) for s in seeds]
+        obs = vec.reset()
+        ref = [oracle_obs_split(spec, o.reset()) for o in orc]
+        for i in range(n):
+            assert np.array_equal(obs["allo"][i].cpu().numpy(), ref[i]["allo"])
+        for t in range(acts.shape[0]):
+            obs, _, _, _ = vec.step(torch.as_tensor(acts[t], dtype=torch.uint8))
+            allo, ego = obs["allo"].cpu().numpy(), obs["ego"].cpu().numpy()
+            ref = [oracle_obs_split(spec, orc[i].step(int(acts[t, i]))[0]) for i in range(n)]
+            for i in range(n):
+                assert np.array_equal(ego[i], ref[i]["ego"])
+                if mode == "1":
+                    assert np.array_equal(allo[i], ref[i]["allo"])
+                else:
+                    poisoned = np.all(allo[i] == 0x55, axis=-1) & np.any(ref[i]["allo"] != 0x55, axis=-1)
+                    frac = poisoned.mean()
+                    assert frac > (0.5 if spec.task == "MoveToRegion" else 0.05), (t, i, frac)
+                    keep = ~np.all(allo[i] == 0x55, axis=-1)
+                    assert np.array_equal(allo[i][keep], ref[i]["allo"][keep])
+        vec.close()
+
+
 @pytest.mark.gpu
 def test_device_sincos_is_correctly_rounded():
     """The device sin/cos (fast certified path + double-double fallback) equals the oracle's
