@@ -471,10 +471,9 @@ MG_DEV int xf_slot(int ent, int x) { return x == MG_XF_MAIN ? ent : SM::RG_MAXE 
 #define RG_SMALL_WPE 7                  // waves per SIMD the small class is compiled for: 72 VGPRs, 9 workgroups/CU
                                         // (measured: 7 -> 2.5% faster than the default 6; 8 = 64 VGPRs slower)
 #endif
-// medium-1 is compiled for 6 waves per SIMD (<= 80 VGPRs): its LDS allows 7 workgroups (21 waves) per CU
 template <class SM, int MODE>
 __global__ void __launch_bounds__(RG_THREADS)
-__attribute__((amdgpu_waves_per_eu((SM::RG_MAXG <= 32 && RG_SMALL_WPE) ? RG_SMALL_WPE : SM::RG_MAXG <= 48 ? 6 : 1)))
+__attribute__((amdgpu_waves_per_eu((SM::RG_MAXG <= 32 && RG_SMALL_WPE) ? RG_SMALL_WPE : 1)))
 render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     __shared__ SM sm;
     constexpr int mode = MODE;
@@ -807,7 +806,12 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     // (its vertex bounds + RG_DMARGIN) and resolves only the others -- bands that no body reaches skip the
     // fill edges, outline lines and resolve altogether.  A block outside every body geom's reach has the
     // same pixels in the full scene as in the static-only scene, so the frame is bit-identical.
-    const bool cview = RG_SCACHE && mode == 0 && view == 0 && out.scache_mode != 1;
+    // (allo frames whose only output is the plain current frame: LoRes4E, LoRes3EA, frames-only; a stacked
+    // allo view writes ring and stack rows in every band anyway, and measured slower with the layer)
+    // The many-block tasks' classes are compiled without it: their scenes' blocks reach most bands, and
+    // the layer's code measured slower there (ClusterColour 2.72 -> 3.00 ms, MatchRegions 3.37 -> 3.41 ms).
+    constexpr bool kLayer = RG_SCACHE && SM::RG_MAXG <= 32;
+    const bool cview = kLayer && mode == 0 && view == 0 && out.scache_mode != 1 && !keep_ring && !stacked && plain;
     const bool mk_cache = cview && fresh && !SM::ORDMAX;
     const bool use_cache = cview && !fresh && S.scache_ok[e] != 0;
     uint8_t *const scache = S.scache + (size_t)e * FR;
@@ -875,7 +879,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     // Allocentric frame whose only output is its plain current frame (LoRes4E, LoRes3EA, frames-only): the
     // bands outside the rows a body geom can reach are the static layer's rows, copied in bulk; the band
     // loop runs over [band0, band1) only.  Elsewhere (frame rings / stacks to write) it runs over every band.
-    const bool brange = use_cache && !keep_ring && !stacked && plain;
+    const bool brange = use_cache;
     auto body_rows = [&](int &b0, int &b1) {   // wave 2: the bands a body geom can reach
         int y0 = MG_RES, y1 = -1;
         for (int g = lane; g < G; g += 64) {
@@ -916,12 +920,12 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
 #endif
     RG_SYNC();
     const int band0 = __builtin_amdgcn_readfirstlane(sm.brng[0]), band1 = __builtin_amdgcn_readfirstlane(sm.brng[1]);
-    if (brange) {   // the static layer's rows outside [band0, band1): 36 x 16 B per band, 2 per thread per round
+    if (brange) {   // the static layer's rows outside [band0, band1): 36 x 16 B per band, 4 per thread per round
         const int nst = (RG_NBANDS - (band1 - band0)) * RG_BANDLO16;
-        for (int i0 = tid; i0 < nst; i0 += 2 * RG_THREADS) {
-            uint4 v[2];
+        for (int i0 = tid; i0 < nst; i0 += 4 * RG_THREADS) {
+            uint4 v[4];
 #pragma unroll
-            for (int k = 0; k < 2; k++) {
+            for (int k = 0; k < 4; k++) {
                 const int i = i0 + k * RG_THREADS;
                 const int b = i / RG_BANDLO16, bb = b < band0 ? b : b + (band1 - band0);
                 const size_t o = (size_t)bb * RG_BANDLO + 16 * (i % RG_BANDLO16);
@@ -929,7 +933,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                 if (out.scache_mode == 2) v[k] = make_uint4(0x55555555u, 0x55555555u, 0x55555555u, 0x55555555u);
             }
 #pragma unroll
-            for (int k = 0; k < 2; k++) {
+            for (int k = 0; k < 4; k++) {
                 const int i = i0 + k * RG_THREADS;
                 const int b = i / RG_BANDLO16, bb = b < band0 ? b : b + (band1 - band0);
                 if (i < nst) *(uint4 *)(o_plain + (size_t)e * FR + (size_t)bb * RG_BANDLO + 16 * (i % RG_BANDLO16)) = v[k];

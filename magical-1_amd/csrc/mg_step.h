@@ -1237,7 +1237,19 @@ MG_DEV bool robot_rows_static(const MGState &S, int e, const GroundRows &G, int 
     return ok;
 }
 
-MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, int lane, MGProf &P) {
+// the sweep's structure (which rows are ground rows, whether the robot rows can run on registers): fixed for
+// an env-step (robot_update changes the motors' rates, not the list), so built once before the 10 substeps
+struct CoopPlan { GroundRows G; int rb0, rc0; bool rstatic; };
+MG_DEV CoopPlan coop_plan(const MGState &S, int lane) {
+    const int e = 0;
+    CoopPlan Q;
+    Q.G = ground_rows(S, e, lane, S.nbodies[e], S.ncons[e]);
+    Q.rb0 = ufirst(S.robot_body0[e]); Q.rc0 = ufirst(S.robot_cons0[e]);
+    Q.rstatic = robot_rows_static(S, e, Q.G, ufirst(S.ncons[e]), Q.rb0, Q.rc0);
+    return Q;
+}
+
+MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, int lane, const CoopPlan &Q, MGProf &P) {
     const int e = 0;
     const uint32_t stamp = S.stamp[e] + 1;
     const double prev_dt = S.curr_dt[e];
@@ -1366,13 +1378,13 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
     }
     const double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
     const int unact = ufirst(nact), unc = ufirst(nc);
-    const GroundRows G = ground_rows(S, e, lane, nb, nc);
+    const GroundRows &G = Q.G;
 #ifndef MG_EXP_COOP_ITERS   // timing experiments only (tools/build_unit_variant.sh)
 #define MG_EXP_COOP_ITERS 10
 #endif
 #ifndef MG_EXP_COOP_NORR   // timing experiments only: the lane-select robot rows below
-    const int rb0 = ufirst(S.robot_body0[e]), rc0 = ufirst(S.robot_cons0[e]);
-    if (robot_rows_static(S, e, G, unc, rb0, rc0)) {
+    const int rb0 = Q.rb0, rc0 = Q.rc0;
+    if (Q.rstatic) {
         RobotV V;
 #pragma unroll
         for (int k = 0; k < 6; k++) {

@@ -158,12 +158,14 @@ __device__ __forceinline__ void env_substeps(const MGState &V, const mg_library 
 __device__ __forceinline__ void env_substeps_coop(const MGState &V, const mg_library *L, int lane, int a, MGProf &P) {
     if (lane == 0) robot_set_action(V, L, 0, a < 18 ? a : 0);
     const double dt = L->dt;
+    __syncthreads();
+    const CoopPlan Q = coop_plan(V, lane);
     for (int i = 0; i < 10; i++) {
         __syncthreads();
         if (lane == 0) robot_update(V, L, 0);
         __syncthreads();
         MG_PP(P, 0);
-        space_step_coop(V, L, dt, lane, P);
+        space_step_coop(V, L, dt, lane, Q, P);
     }
 }
 

@@ -471,7 +471,7 @@ def test_reset_paths(name, n, steps, L, env, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,n", [("MoveToRegion-Demo-LoRes4E-v0", 64), ("MatchRegions-TestAll-LoRes4E-v0", 64)])
+@pytest.mark.parametrize("name,n", [("MoveToRegion-Demo-LoRes4E-v0", 64), ("MoveToCorner-Demo-LoRes4E-v0", 64)])
 def test_allo_static_layer_in_use(name, n, monkeypatch):
     """The allocentric static layer (render_kernel: arena + goals rendered once per episode, copied into
     every 4x4 block no body geom reaches) is really used: with its copied blocks poisoned
@@ -500,7 +500,7 @@ def test_allo_static_layer_in_use(name, n, monkeypatch):
                 else:
                     poisoned = np.all(allo[i] == 0x55, axis=-1) & np.any(ref[i]["allo"] != 0x55, axis=-1)
                     frac = poisoned.mean()
-                    assert frac > (0.5 if spec.task == "MoveToRegion" else 0.05), (t, i, frac)
+                    assert frac > 0.3, (t, i, frac)
                     keep = ~np.all(allo[i] == 0x55, axis=-1)
                     assert np.array_equal(allo[i][keep], ref[i]["allo"][keep])
         vec.close()
