@@ -120,3 +120,38 @@ def random_policy(num_envs, device="cuda:0", seed=0):
     gen = torch.Generator(device=device)
     gen.manual_seed(seed)
     return lambda obs: torch.randint(0, 18, (num_envs,), generator=gen, device=device, dtype=torch.int64).to(torch.uint8)
+
+
+def latexify_results(eval_data, id_column="run_id"):
+    """evaluation.py:101-154: a LaTeX table of a `do_eval()` frame (or of several runs' frames
+    concatenated): one column per test env (in order of first appearance), one row per value of
+    `id_column`, cells "mean ($\\pm$ std)" with two decimals.  Same text as the reference, including its
+    layout quirk of closing the tabular after every algorithm row; a (run, env) pair that is not exactly
+    one record raises ValueError with the reference's message."""
+    rows = eval_data.to_dict("records") if hasattr(eval_data, "to_dict") else list(eval_data)
+
+    def unique(key):
+        seen = []
+        for r in rows:
+            if r[key] not in seen:
+                seen.append(r[key])
+        return seen
+
+    test_envs, alg_names = unique("test_env"), unique(id_column)
+    col_names = [r"\textbf{%s}" % e for e in test_envs]
+    out = [r"\centering" + "\n", r"\begin{tabular}{l@{\hspace{1em}}%s}" % ("c" * len(col_names)) + "\n",
+           r"\toprule" + "\n", r"\textbf{Randomisation} & " + " & ".join(col_names) + "\\\\\n", r"\midrule" + "\n"]
+    for alg_name in alg_names:
+        stat_parts = []
+        for env_name in test_envs:
+            match = [r for r in rows if r[id_column] == alg_name and r["test_env"] == env_name]
+            if len(match) != 1:
+                raise ValueError(f"got {len(match)} rows corresponding to {id_column}={alg_name} and "
+                                 f"test_env={env_name}, but expected one (maybe IDs in column {id_column} "
+                                 f"aren't unique?)")
+            row = match[0]
+            stat_parts.append(f'{row["mean_score"]:.2f} ($\\pm$ {row["std_score"]:.2f})')
+        out.append(r"\textbf{%s} & " % alg_name + " & ".join(stat_parts) + "\\\\\n")
+        out.append(r"\bottomrule" + "\n")
+        out.append(r"\end{tabular}" + "\n")
+    return "".join(out)

@@ -37,6 +37,7 @@ written out: the JSON files hold inputs and the reference's outputs only.
                         are stand-ins (cv2 INTER_AREA 4x = the oracle's
                         o_downsample, pinned separately).  Stored: observation
                         keys, shapes, dtypes and a sha256 per value and event.
+  * ref_latex.json    -- evaluation.py:101-154 (latexify_results) on synthetic do_eval() frames.
   * ref_scorers.json  -- cluster.py:166-216 (BaseClusterEnv.score_on_end_of_traj)
                         on random, clustered and near-threshold block layouts;
                         move_to_corner.py:67-100 (score_on_end_of_traj and
@@ -458,11 +459,36 @@ def ref_actions():
     return {"actions": rows, "flag_values": {m.name: int(m.value) for m in ns["RobotAction"]}}
 
 
+def ref_latex():
+    """evaluation.py:101-154 (latexify_results) on synthetic do_eval() frames: one and two algorithms over
+    a demo env and its test variants, env order as first seen; plus the duplicate-id error message."""
+    import io
+    import pandas as pd
+    ns = {"io": io}
+    _extract(os.path.join(REF, "evaluation.py"), ["latexify_results"], ns)
+    rs = np.random.RandomState(77)
+    envs = ["MoveToCorner-Demo-v0", "MoveToCorner-TestJitter-v0", "MoveToCorner-TestColour-v0", "MoveToCorner-TestAll-v0"]
+    cases = []
+    for algs, col in ((["bc"], "run_id"), (["bc", "gail", "dagger"], "run_id"), (["x", "y"], "algo")):
+        recs = [{"demo_env": envs[0], "test_env": e, "mean_score": float(rs.uniform(0, 1)),
+                 "std_score": float(rs.uniform(0, 0.5)), col: a} for a in algs for e in envs]
+        cases.append({"records": recs, "id_column": col,
+                      "latex": ns["latexify_results"](pd.DataFrame.from_records(recs), id_column=col)})
+    dup = cases[0]["records"] + cases[0]["records"][:1]
+    try:
+        ns["latexify_results"](pd.DataFrame.from_records(dup))
+        err = None
+    except ValueError as ex:
+        err = str(ex)
+    return {"cases": cases, "duplicate": {"records": dup, "error": err}}
+
+
 def main():
     only = set(sys.argv[1:])
     for fn, make in (("ref_render.json", ref_render), ("ref_make_line.json", ref_make_line),
                      ("ref_outline.json", ref_outline), ("ref_wrappers.json", ref_wrappers),
-                     ("ref_scorers.json", ref_scorers), ("ref_actions.json", ref_actions)):
+                     ("ref_scorers.json", ref_scorers), ("ref_actions.json", ref_actions),
+                     ("ref_latex.json", ref_latex)):
         if only and fn not in only:
             continue
         data = make()

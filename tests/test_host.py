@@ -402,3 +402,20 @@ def test_evaluation_protocol_statistics():
     import pytest
     with pytest.raises(ValueError):
         Short("MoveToCorner-Demo-v0", 10).do_eval()
+
+
+def test_latexify_results_matches_reference():
+    """evaluation.py:101-154 latexify_results: the text the reference's own function produced
+    (tests/golden/ref_latex.json, make_ref_fixtures.py) for one- and multi-algorithm frames and a custom
+    id column, and its error on a duplicated (run, env) record."""
+    import json
+    import pandas as pd
+    import pytest
+    from magical_amd import evaluation
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "ref_latex.json")))
+    for case in ref["cases"]:
+        frame = pd.DataFrame.from_records(case["records"])
+        assert evaluation.latexify_results(frame, id_column=case["id_column"]) == case["latex"]
+    with pytest.raises(ValueError) as ei:
+        evaluation.latexify_results(pd.DataFrame.from_records(ref["duplicate"]["records"]))
+    assert str(ei.value) == ref["duplicate"]["error"]
