@@ -318,7 +318,10 @@ MG_DEV void contact_points(const Edge &e1, const Edge &e2, const Closest &pts, C
 }
 
 // cpCollide: (a, b) are swapped so type(a) <= type(b); returns swapped flag
-MG_DEV bool collide(const ShapeW &A, const ShapeW &B, Collision &info) {
+#ifndef MG_COLLIDE_ATTR
+#define MG_COLLIDE_ATTR MG_DEV
+#endif
+MG_COLLIDE_ATTR bool collide(const ShapeW &A, const ShapeW &B, Collision &info) {
     info.count = 0; info.n = v2(0, 0);
     bool sw = A.type > B.type;
     const ShapeW &a = sw ? B : A;

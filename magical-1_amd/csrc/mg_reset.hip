@@ -1,4 +1,7 @@
 // mg_reset.hip -- seed (MT19937 per env) and reset (BaseEnv.reset + on_reset, masked) kernels.
+// the reset is off the step path (next-layout shadow): one out-of-line collide()
+// for its shape queries keeps this unit's compile time bounded (about 1 min instead of 35+)
+#define MG_COLLIDE_ATTR __device__ __attribute__((noinline))
 #include "mg_launch.h"
 #include "mg_reset.h"
 __global__ void __launch_bounds__(64) seed_kernel(MGState S, const uint32_t *__restrict__ seeds) {

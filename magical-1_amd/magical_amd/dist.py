@@ -23,10 +23,12 @@ the whole node's step results -- is one all-gather per step:
   restarts its stacks: its frame is the next episode's first).  The simulator
   binds its outputs in frames-only mode, so it writes no stacks of its own.
   gather_mode "stacked" gathers the preprocessor's whole outputs instead;
-* two buffer sets alternate between steps and the collective (then the
-  restack) runs on its own HIP stream, so the exchange of step t overlaps the
-  compute of step t + 1 (ShardedVecEnv.step_async).  A step's gathered views
-  stay valid until the step after next.
+* two buffer sets alternate between steps; the collective runs on its own HIP
+  stream and the restack on a third (in step order), so the exchange of step t
+  overlaps the compute of step t + 1 and the restack of step t (HBM-bound)
+  overlaps the all-gather of step t + 1 (xGMI-bound)
+  (ShardedVecEnv.step_async).  A step's gathered views stay valid until the
+  step after next.
 """
 import collections
 
@@ -239,6 +241,9 @@ class ShardedVecEnv:
             self.restacker = restacker
             self.pending = [None, None]
             self.comm_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+            # the restack has its own stream: restack(t) (HBM-bound) overlaps gather(t + 1) (xGMI-bound)
+            self.restack_stream = torch.cuda.Stream(dev) if dev.type == "cuda" and frames else None
+            self.restacked = [None, None]   # per buffer set: event after the restack that last read recv[b]
             self.t = 0
 
     # -- packed gather pipeline ---------------------------------------------------------------------------
@@ -264,11 +269,17 @@ class ShardedVecEnv:
             ev = torch.cuda.current_stream(self.device).record_event()
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
+                if self.restacked[b] is not None:   # the restack of step t - 2 has read recv[b]
+                    self.comm_stream.wait_event(self.restacked[b])
                 work = dist.all_gather_into_tensor(recv, send, async_op=True)
                 work.wait()   # the side stream (not the host) waits for the collective
-                if stacks is not None:
-                    self.restacker(recv, stacks, step, all_fresh)
                 done_ev = self.comm_stream.record_event()
+            if stacks is not None:
+                # in step order on its own stream (the receive ring carries state from step to step)
+                with torch.cuda.stream(self.restack_stream):
+                    self.restack_stream.wait_event(done_ev)
+                    self.restacker(recv, stacks, step, all_fresh)
+                    done_ev = self.restacked[b] = self.restack_stream.record_event()
             h = GatheredStep(self.layout, recv, stacks, event=done_ev)
         else:
             work = dist.all_gather_into_tensor(recv, send, async_op=True)
