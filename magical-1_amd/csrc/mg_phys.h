@@ -293,8 +293,11 @@ MG_DEV Edge support_edge_segment(const ShapeW &sh, V2 n) {
     return {sh.b, sh.a, hash_pair(sh.hashid, 1), hash_pair(sh.hashid, 0), sh.r};
 }
 MG_DEV void push_contact(Collision &c, V2 p1, V2 p2, uint64_t h) {
+    // constant indices (a run-time index puts the whole Collision in per-lane scratch memory)
     if (c.count >= 2) return;
-    c.p1[c.count] = p1; c.p2[c.count] = p2; c.hash[c.count] = h; c.count++;
+    if (c.count == 0) { c.p1[0] = p1; c.p2[0] = p2; c.hash[0] = h; }
+    else { c.p1[1] = p1; c.p2[1] = p2; c.hash[1] = h; }
+    c.count++;
 }
 MG_DEV void contact_points(const Edge &e1, const Edge &e2, const Closest &pts, Collision &info) {
     double mindist = e1.r + e2.r;

@@ -45,7 +45,7 @@ bool mg_step_blk_ok(int variant, int blk) {
     return variant == 0 ? (blk == 1 || blk == 8 || blk == 64)
          : variant == 3 ? (blk == 1 || blk == 4)
          : variant == 4 ? blk == 1
-         : variant == 5 || variant == 6 ? blk == 16
+         : variant == 5 || variant == 6 ? (blk == 4 || blk == 8 || blk == 16)
          : (blk == 1 || blk == 4 || blk == 16);
 }
 
@@ -58,7 +58,7 @@ hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, in
     MG_STEP_CASE(1, 1) MG_STEP_CASE(1, 4) MG_STEP_CASE(1, 16)
     MG_STEP_CASE(2, 1) MG_STEP_CASE(2, 4) MG_STEP_CASE(2, 16)
     MG_STEP_CASE(3, 1) MG_STEP_CASE(3, 4) MG_STEP_CASE(4, 1)
-    MG_STEP_CASE(5, 16) MG_STEP_CASE(6, 16)
+    MG_STEP_CASE(5, 16) MG_STEP_CASE(6, 16) MG_STEP_CASE(5, 8) MG_STEP_CASE(6, 8) MG_STEP_CASE(5, 4) MG_STEP_CASE(6, 4)
     MG_STEP_CASE(0, 1) MG_STEP_CASE(0, 8) MG_STEP_CASE(0, 64)
 #undef MG_STEP_CASE
     return hipErrorInvalidValue;

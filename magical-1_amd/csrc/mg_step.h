@@ -266,7 +266,9 @@ MG_DEV void arbiter_update_t(const MGState &S, const mg_library *L, int e, int k
     uint64_t oh0 = AHASH(0, slot), oh1 = AHASH(1, slot);
     double ojn0 = ACON(0, AC_JN, slot), ojt0 = ACON(0, AC_JT, slot);
     double ojn1 = ACON(1, AC_JN, slot), ojt1 = ACON(1, AC_JT, slot);
-    for (int k = 0; k < info.count; k++) {
+#pragma unroll
+    for (int k = 0; k < 2; k++) {   // constant indices: the Collision can stay in registers
+        if (k >= info.count) break;
         V2 r1 = vsub(info.p1[k], pa), r2 = vsub(info.p2[k], pb);
         double jn = 0.0, jt = 0.0;
         uint64_t h = info.hash[k];

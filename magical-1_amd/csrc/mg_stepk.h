@@ -10,10 +10,10 @@
 #include "mg_score.h"
 
 // slot caps of every compiled form: the LDS variants of mg_launch.h, plus the QL-lanes-per-env forms of the
-// compile-time scenes (5: the caps of 1 with two world-shape slots per lane in LDS; 6: the caps of 2, world
-// shapes in per-lane locals as there)
-__host__ __device__ constexpr StepCaps step_form_caps(int v) {
-    return v == 5 ? StepCaps{6, 5, 10, 20, 16, 8} : v == 6 ? StepCaps{7, 6, 12, 32, 16, 0} : step_variant_caps(v);
+// compile-time scenes (5: the caps of 1 with two world-shape slots per lane in LDS -- 2 x 64 per workgroup,
+// so 128 / blk per env; 6: the caps of 2, world shapes in per-lane locals as there)
+__host__ __device__ constexpr StepCaps step_form_caps(int v, int blk) {
+    return v == 5 ? StepCaps{6, 5, 10, 20, 16, 128 / blk} : v == 6 ? StepCaps{7, 6, 12, 32, 16, 0} : step_variant_caps(v);
 }
 
 // ---- LDS-resident substeps ------------------------------------------------
@@ -174,7 +174,7 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
                                                   int auto_reset, const uint8_t *__restrict__ actions, float *reward,
                                                   uint8_t *done, double *eval_score, uint8_t *reset_mask) {
     extern __shared__ __align__(16) unsigned char smem[];
-    constexpr StepCaps C = step_form_caps(VAR);
+    constexpr StepCaps C = step_form_caps(VAR, BLK);
     constexpr bool LDS = VAR != 0;
     constexpr bool COOP = VAR == 4;            // one env per workgroup of 64 lanes
     constexpr bool QUAD = VAR == 5 || VAR == 6; // QL lanes per env, BLK envs in one 64-lane workgroup
@@ -262,7 +262,7 @@ template <int VAR, int BLK>
 hipError_t launch_step_var(const MGState &S, const mg_library *L, TaskCfg cfg, int max_steps, int auto_reset,
                                   const uint8_t *actions, float *reward, uint8_t *done, double *eval_score,
                                   uint8_t *reset_mask, hipStream_t st) {
-    constexpr StepCaps C = step_form_caps(VAR);
+    constexpr StepCaps C = step_form_caps(VAR, BLK);
     const size_t lds = VAR == 0 ? 0 : mg_step_lds_bytes(C, BLK);
     static bool attr_set = false;
     if (VAR != 0 && !attr_set) {
