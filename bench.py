@@ -42,6 +42,18 @@ FR = 96 * 96 * 3            # one LoRes RGB frame
 STATE_BYTES = 2048          # per-env state read + written once per env-step (~2 KB)
 
 
+def survey_bytes(preproc):
+    """SURVEY.md 8(d) algorithmic bytes of one env-step: the observation outputs + ~2 KB of state
+    (LoRes4E family 167 936 B, LoResStack 223 232 B).  roofline.frac uses these for every kernel."""
+    return obs_bytes(preproc) + STATE_BYTES
+
+
+def kernel_survey_bytes(kernel, preproc):
+    """The share of survey_bytes a kernel is charged in roofline.traffic_ratio: the render kernel writes the
+    observations (+ the nominal state, as 8(d) counts the env-step), the step kernel reads + writes the state."""
+    return survey_bytes(preproc) if kernel == "render_kernel" else STATE_BYTES
+
+
 def obs_bytes(preproc):
     return {"LoRes4E": 165888, "LoRes4A": 165888, "LoRes3EA": 165888, "LoResCHW4E": 165888, "LoResCHW4A": 165888,
             "LoResStack": 221184}.get(preproc, 2 * 384 * 384 * 3)
@@ -151,6 +163,15 @@ def load_pmc(kernel, workload, envs):
     return None
 
 
+CPU_ENV = "MAGICAL_BENCH_CPU_BASELINE"   # launcher parent -> rank 0: the measured cpu_baseline object (JSON)
+
+
+def measure_cpu_baseline(args):
+    share, affinity, quota = cpu_share()
+    workers = args.cpu_workers or share
+    return cpu_baseline(args.env, workers, args.cpu_steps, affinity, quota)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -167,14 +188,28 @@ def launch_ranks(n):
     return subprocess.call(cmd, env=dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1")))
 
 
-def kernel_record(name, ms, bytes_per_env, n, pmc):
-    """One kernel's roofline figures: algorithmic bytes per launch over its HIP-event average duration."""
+def kernel_record(name, ms, preproc, n, pmc, frames_only=False):
+    """One kernel's roofline figures over its HIP-event average duration (ms per launch, one launch per step):
+    * achieved / hbm_frac: SURVEY 8(d) bytes of the env-steps the launch completes (survey_bytes x n);
+    * traffic_ratio: PMC HBM bytes per launch (committed rocprofv3 FETCH/WRITE passes of the same workload
+      and env count) over the kernel's own 8(d) share x n (render: obs + state, step: state);
+    * kernel_bytes_*: the bytes this kernel must move by its design (render: obs + the frame ring's reads
+      and writes; step: state) -- the ring-inclusive figure of earlier rounds."""
     if ms is None or ms <= 0:
         return None
-    ach = bytes_per_env * n / (ms * 1e-3) / 1e9
-    return {"ms": round(ms, 4), "bytes_per_env_step": bytes_per_env, "achieved_gbs": round(ach, 2),
+    sb = survey_bytes(preproc)
+    ach = sb * n / (ms * 1e-3) / 1e9
+    kb = render_bytes(preproc, frames_only) if name == "render_kernel" else STATE_BYTES
+    kach = kb * n / (ms * 1e-3) / 1e9
+    traffic = pmc and pmc.get("bytes_per_launch")
+    share = kernel_survey_bytes(name, preproc)
+    return {"ms": round(ms, 4), "bytes_per_env_step": sb, "achieved_gbs": round(ach, 2),
             "hbm_frac": round(ach / HBM_PEAK_GBS, 5),
-            "traffic_bytes_per_launch": pmc and pmc.get("bytes_per_launch"),
+            "traffic_bytes_per_launch": traffic,
+            "traffic_ratio": round(traffic / (share * n), 2) if traffic else None,
+            "traffic_ratio_basis_bytes_per_env_step": share,
+            "kernel_bytes_per_env_step": kb, "kernel_bytes_achieved_gbs": round(kach, 2),
+            "kernel_bytes_hbm_frac": round(kach / HBM_PEAK_GBS, 5),
             "valu_issue_frac": pmc and pmc.get("valu_issue_frac"), "wait_any_frac": pmc and pmc.get("wait_any_frac")}
 
 
@@ -199,12 +234,24 @@ def main():
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the CPU baseline is measured here, in the launcher parent, before any rank (or GPU) exists; rank 0
+        # puts it on its line
+        if not args.no_cpu_baseline:
+            os.environ[CPU_ENV] = json.dumps(measure_cpu_baseline(args))
         sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:   # an outside launcher decides the world size; --gpus is informational then
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; using {world} ranks", file=sys.stderr)
+
+    # rank 0's CPU baseline: from the launcher parent when bench.py launched the ranks, else measured here
+    # before this process touches a GPU (an outside torch.distributed.run: the other ranks wait in the
+    # process-group rendezvous meanwhile)
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = json.loads(os.environ[CPU_ENV]) if os.environ.get(CPU_ENV) else measure_cpu_baseline(args)
+        cpu["measured_in"] = "launcher parent" if os.environ.get(CPU_ENV) else "rank 0 before GPU init"
 
     if args.dry_run:
         import torch
@@ -216,16 +263,11 @@ def main():
             dist.all_reduce(t)
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": args.gpus, "ranks_seen": int(t.item()),
-                              "gather": args.gather if args.gather is not None else world > 1}), flush=True)
+                              "gather": args.gather if args.gather is not None else world > 1,
+                              "cpu_baseline": cpu}), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        share, affinity, quota = cpu_share()
-        workers = args.cpu_workers or share
-        cpu = cpu_baseline(args.env, workers, args.cpu_steps, affinity, quota)
 
     import torch
     import torch.distributed as dist
@@ -297,9 +339,9 @@ def main():
     if rank == 0:
         frames_only = gather and args.gather_mode == "frames"
         kernels = {
-            "render_kernel": kernel_record("render_kernel", t_render_ms, render_bytes(spec.preproc, frames_only), n,
-                                           load_pmc("render_kernel", args.env, n)),
-            "step_kernel": kernel_record("step_kernel", t_step_ms, STATE_BYTES, n, load_pmc("step_kernel", args.env, n)),
+            "render_kernel": kernel_record("render_kernel", t_render_ms, spec.preproc, n,
+                                           load_pmc("render_kernel", args.env, n), frames_only),
+            "step_kernel": kernel_record("step_kernel", t_step_ms, spec.preproc, n, load_pmc("step_kernel", args.env, n)),
             "reset_kernel": {"ms": round(t_reset_ms, 4)},
         }
         dom = "render_kernel" if t_render_ms >= t_step_ms else "step_kernel"
@@ -324,12 +366,20 @@ def main():
                        "parallelism": (f"dp{world} (envs sharded; one packed all-gather per step ({args.gather_mode}), "
                                        f"pipelined with the next step)" if gather else
                                        f"dp{world} (envs sharded, no data-path collective)")},
-            # dominant kernel against HBM with ITS OWN algorithmic bytes (render: observations + frame ring;
-            # step: SURVEY 8(d) state bytes); the binding resource of both is VALU issue / latency
+            # dominant kernel against HBM with SURVEY 8(d)'s bytes per env-step x the envs one launch
+            # completes; traffic_ratio = its PMC bytes per launch over its own 8(d) share (render: obs + state,
+            # step: state); the ring-inclusive bytes of the render kernel's design under "kernel_bytes"; the
+            # binding resource of both kernels is VALU issue / latency
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": dk["achieved_gbs"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": dk["hbm_frac"], "traffic": dk["traffic_bytes_per_launch"],
+                         "traffic_ratio": dk["traffic_ratio"],
+                         "traffic_ratio_basis_bytes_per_env_step": dk["traffic_ratio_basis_bytes_per_env_step"],
                          "bytes_per_env_step": dk["bytes_per_env_step"], "units_per_launch": n,
-                         "kernel_avg_ms": dk["ms"], "binding": "valu_issue_latency",
+                         "kernel_avg_ms": dk["ms"],
+                         "kernel_bytes": {"bytes_per_env_step": dk["kernel_bytes_per_env_step"],
+                                          "achieved": dk["kernel_bytes_achieved_gbs"],
+                                          "frac": dk["kernel_bytes_hbm_frac"]},
+                         "binding": "valu_issue_latency",
                          "valu_issue_frac": dk["valu_issue_frac"], "wait_any_frac": dk["wait_any_frac"]},
             "kernels": kernels,
             "kernel_ms_per_step": {"step_kernel": round(t_step_ms, 4), "reset_kernel": round(t_reset_ms, 4),

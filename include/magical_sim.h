@@ -87,7 +87,9 @@ int mg_set_body_pose(mg_sim *sim, int env, int body, double x, double y, double 
  * far (sticky), 4 / 8 allo / ego raster assumption or capacity, 16 / 32 scene outside the step kernel's
  * compiled caps / constraint list */
 int mg_get_errors(mg_sim *sim, int32_t *out_dev, void *stream);
-/* re-seed env RNGs (env.seed): host u32[num_envs] */
+/* re-seed env RNGs (env.seed): host u32[num_envs].  The many-block tasks' next-layout shadow (layouts drawn
+ * ahead on an internal stream) is invalidated: auto-resets run in place on the caller's stream until the next
+ * full (mask == NULL) mg_reset re-primes it -- same results, slower resets. */
 int mg_seed(mg_sim *sim, const uint32_t *seeds_host);
 /* device-side uniform random actions for throughput runs (Philox 4x32-10, key, counter = (step, env)) */
 int mg_random_actions(mg_sim *sim, uint8_t *actions_dev, uint64_t key, uint64_t step, void *stream);
@@ -119,7 +121,8 @@ int mg_replay_lores(const uint8_t *frames, int32_t nframes, const int32_t *episo
  * recv: device u8, `world` rank blocks of rank_stride bytes; block r holds env r*n+i's current allo frame
  * u8[96,96,3] at off_allo + i*27648, its ego frame at off_ego + i*27648 and its done flag u8 at off_done + i
  * (all offsets 16-byte aligned, as the frames-only outputs of mg_bind_outputs write them).
- * ring: device u8[2][4][world*n][27648], caller-owned and persistent across calls (step t writes slot t % 4).
+ * ring: device u8[stacks][4][world*n][27648], stacks = 2 for LoResStack (allo, ego), else 1 (the view the
+ * stacked output is built from), caller-owned and persistent across calls (step t writes slot t % 4).
  * all_fresh = 1 after a reset of every env; otherwise an env whose done flag is set restarts its stacks
  * (auto-reset: its frame is the next episode's first).  Outputs for world*n envs, as mg_buffers' stacked
  * outputs: preproc 1 (LoRes4E / CHW4E / CHW4A), 3 (LoRes3EA), 4 (LoRes4A): out_past u8[world*n,96,96,12]

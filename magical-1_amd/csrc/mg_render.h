@@ -480,6 +480,10 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     const int e = blockIdx.x, view = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
     if (e >= S.n_envs || (out.mask && !out.mask[e])) return;
     if (out.retry_in && !S.rg_retry[2 * e + view]) return;
+    // an episode's first allo frame invalidates the static layer of the previous episode before anything can
+    // fail: a frame that a class hands over (or gives up on) must not leave the old layer marked valid
+    // (ADVICE r3); a successful first frame of the layer's class sets it again at the end
+    if (MODE == 0 && view == 0 && tid == 0 && S.scache_ok && S.episode_steps[e] == 0) S.scache_ok[e] = 0;
     MG_PROF_BEGIN(tid == 0);
     // capacity overflow: a class with a successor hands the (env, view) to it, else an env error
 #define RG_FAIL() do { \

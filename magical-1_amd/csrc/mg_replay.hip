@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void restack_kernel(const uint8_t *__restrict_
     const int rv = (preproc == MG_PREPROC_LORES4A || (preproc == MG_PREPROC_LORESSTACK && s == 0)) ? 0 : 1;
     const size_t po = (size_t)q * 12;
     const uint32_t *cur = (const uint32_t *)(blk + (rv ? off_e : off_a) + (size_t)i * LOFR + po);
-    uint8_t *rring = ring + (size_t)rv * 4 * W * LOFR;
+    uint8_t *rring = ring + (size_t)s * 4 * W * LOFR;   // one ring per output stack (LoResStack: 2, else 1)
     auto rslot = [&](uint32_t sl) { return (uint32_t *)(rring + ((size_t)(sl & 3) * W + g) * LOFR + po); };
     uint32_t f[4][3];
 #pragma unroll

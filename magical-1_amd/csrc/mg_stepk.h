@@ -229,6 +229,10 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
             }
             env_substeps_quad<NCS, QL, (C.shw > 0)>(V, L, lane, sub, a, P);
             if (own) xfer_state(S, V, C, lane, e, false, false, sub, QL);
+            // the env's lane 0 scores from HBM rows its sibling lanes just wrote back: order them
+            // by the memory model, not by one wavefront's in-order memory pipe
+            __threadfence_block();
+            __syncthreads();
             if (!own || sub != 0) return;
         } else if constexpr (COOP) {
             xfer_state(S, V, C, 0, e, true, true, lane, 64);

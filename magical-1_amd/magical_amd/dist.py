@@ -134,16 +134,29 @@ class PackedLayout:
         return out
 
 
+def restack_ring_bytes(preproc, world, n):
+    """Bytes of mg_restack's receive ring: the last 4 frames of every stacked output's view for all W * n envs,
+    u8[stacks][4][W * n][96 * 96 * 3] (LoResStack: 2 stacks, allo and ego; else 1)."""
+    return len(stacked_keys(preproc)) * 4 * world * n * LOFR
+
+
+def frames_mode_bytes(preproc, world, n):
+    """Receiver-side device memory of gather_mode 'frames' per rank: the ring plus two sets of rebuilt
+    stacks (u8[W * n][96][96][12] per stacked key, one set per alternating buffer set)."""
+    return restack_ring_bytes(preproc, world, n) + 2 * len(stacked_keys(preproc)) * world * n * 4 * LOFR
+
+
 class NativeRestacker:
     """Receiver-side frame stacks of the frames-only gather on the GPU (mg_restack): keeps a ring of the
-    last 4 frames of each view for all W * n envs, u8[2][4][W * n][96 * 96 * 3]."""
+    last 4 frames of each stacked output's view for all W * n envs (restack_ring_bytes)."""
 
     def __init__(self, layout, world, device):
         from . import native
         self.lib, self.native = native.load(), native
         self.layout, self.world = layout, world
         self.preproc = GPU_PREPROC[layout.preproc]
-        self.ring = torch.empty(2 * 4 * world * layout.n * LOFR, dtype=torch.uint8, device=device)
+        self.ring = torch.empty(restack_ring_bytes(layout.preproc, world, layout.n), dtype=torch.uint8,
+                                device=device)
         self.off = (layout.offset("allo"), layout.offset("ego"), layout.offset("done"))
 
     def __call__(self, recv, outs, step, all_fresh):
@@ -200,12 +213,15 @@ class ShardedVecEnv:
 
     gather=True: every step's results of all ranks reach every rank (see the module docstring); step()
     returns the gathered [W, n, ...] views, step_async() the handle without waiting, so the exchange of
-    step t overlaps step t + 1.  gather_mode 'frames' (default) all-gathers only the current frames and
-    rebuilds the stacks on each receiver (`restacker`: NativeRestacker on the GPU; CPU tensors need one
-    passed in -- the gloo tests use the oracle's); 'stacked' all-gathers the whole observations."""
+    step t overlaps step t + 1.  gather_mode 'frames' (default on GPU tensors) all-gathers only the current
+    frames and rebuilds the stacks on each receiver (`restacker`: NativeRestacker on the GPU; CPU tensors need
+    one passed in -- the gloo tests use the oracle's); 'stacked' (default on CPU tensors) all-gathers the
+    whole observations.  In 'frames' mode the receivers' rings are valid only from reset_async() on:
+    step_async() raises before the shard's first reset_async() and after the VecMagicalEnv underneath was
+    reset directly (vec.reset()), since the other ranks' rings would then hold stale frames of its envs."""
 
     def __init__(self, env_name, envs_per_rank, rank=None, device=None, base_seed=1000, gather=False, vec=None,
-                 gather_mode="frames", restacker=None, max_episode_steps=None):
+                 gather_mode=None, restacker=None, max_episode_steps=None):
         from . import registry
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if dist.is_initialized() else 1
@@ -219,13 +235,15 @@ class ShardedVecEnv:
                                 max_episode_steps=max_episode_steps)
         self.vec = vec
         if gather:
+            dev = torch.device(device) if device is not None else getattr(vec, "device", torch.device("cpu"))
+            if gather_mode is None:
+                gather_mode = "frames" if dev.type == "cuda" or restacker is not None else "stacked"
             if gather_mode not in ("frames", "stacked"):
                 raise ValueError(f"gather_mode must be 'frames' or 'stacked', not {gather_mode!r}")
             self.gather_mode = gather_mode
             frames = gather_mode == "frames"
             self.layout = PackedLayout.for_spec(spec, envs_per_rank, frames_only=frames)
             self.stacked_nbytes = PackedLayout.for_spec(spec, envs_per_rank).nbytes
-            dev = torch.device(device) if device is not None else getattr(vec, "device", torch.device("cpu"))
             self.device = dev
             self.send = [torch.empty(self.layout.nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
             self.recv = [torch.empty(self.world * self.layout.nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -245,6 +263,7 @@ class ShardedVecEnv:
             self.restack_stream = torch.cuda.Stream(dev) if dev.type == "cuda" and frames else None
             self.restacked = [None, None]   # per buffer set: event after the restack that last read recv[b]
             self.t = 0
+            self._ring_resets = None        # vec.reset_count at the last reset_async (frames mode: ring valid)
 
     # -- packed gather pipeline ---------------------------------------------------------------------------
     def _begin(self):
@@ -294,10 +313,18 @@ class ShardedVecEnv:
     def reset_async(self):
         b = self._begin()
         self.vec.reset()
+        self._ring_resets = getattr(self.vec, "reset_count", None)
         self._finish_outputs(b)
         return self._launch(b, all_fresh=True)
 
     def step_async(self, actions):
+        if self.layout.frames_only:   # never restack from an unfilled or stale ring
+            if self._ring_resets is None and self.t == 0:
+                raise RuntimeError("ShardedVecEnv(gather_mode='frames'): call reset() / reset_async() before the "
+                                   "first step (the receivers' frame rings are filled by it)")
+            if getattr(self.vec, "reset_count", None) != self._ring_resets:
+                raise RuntimeError("ShardedVecEnv(gather_mode='frames'): the VecMagicalEnv was reset directly; "
+                                   "reset through reset() / reset_async() so every rank's frame ring restarts")
         b = self._begin()
         self.vec.step(actions)
         self._finish_outputs(b)

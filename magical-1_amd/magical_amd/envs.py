@@ -118,6 +118,7 @@ class VecMagicalEnv:
         self.eval_score = torch.zeros(n, dtype=torch.float64, device=dev)
         self.target = torch.zeros((n, 4), dtype=torch.float64, device=dev) if self.spec.task == "PickAndPlace" else None
         self.frames_only = False
+        self.reset_count = 0   # explicit reset() calls (magical_amd.dist checks its frame rings against it)
         self._bind()
         self.action_space = spaces.Discrete(18)
         self.observation_space = observation_space(self.spec)
@@ -183,6 +184,7 @@ class VecMagicalEnv:
     def reset(self, mask=None):
         m = None if mask is None else ctypes.c_void_p(mask.to(self.device, torch.uint8).contiguous().data_ptr())
         native.check(self.lib.mg_reset(self.handle, m, self._stream()))
+        self.reset_count += 1
         if self.spec.preproc is None:
             self.render_full(out=self.full)
         return self._obs()

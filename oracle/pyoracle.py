@@ -69,6 +69,9 @@ def lib():
         L.oenv_get_phys_vars.argtypes = [vp, vp]
         L.o_palette.argtypes = [vp]
         L.o_downsample.argtypes = [vp, vp]
+        L.osc_entity.argtypes = [vp, i, vp]
+        L.osc_get_pose.argtypes = [vp, i, i, vp]
+        L.oenv_get_rng.argtypes = [vp, vp, vp]
         _lib = L
     return _lib
 
@@ -185,6 +188,29 @@ class OracleEnv:
 
     def num_arbiters(self):
         return self.L.oenv_num_arbiters(self.h)
+
+    def entity_poses(self):
+        """per entity after the arena, in add order: (x, y, angle) of each of its bodies (the goal: its static
+        body's position, angle 0) -- tests/golden/ref_resets.json's layout"""
+        n = len(self.entities()[0])
+        out = []
+        for ent in range(1, n):
+            d = np.zeros(5, dtype=np.int32)
+            self.L.osc_entity(self.h, ent, ptr(d))
+            poses = []
+            for k in range(int(d[2])):
+                p = np.zeros(3)
+                self.L.osc_get_pose(self.h, ent, k, ptr(p))
+                poses.append(p.tolist())
+            out.append(poses)
+        return out
+
+    def rng_state(self):
+        """(key u32[624], pos) of the env's MT19937 -- numpy RandomState.get_state()[1:3]"""
+        key = np.zeros(624, dtype=np.uint32)
+        pos = ctypes.c_int()
+        self.L.oenv_get_rng(self.h, ptr(key), ctypes.byref(pos))
+        return key, pos.value
 
     def entities(self):
         k = np.zeros(32, dtype=np.int32)

@@ -1454,3 +1454,88 @@ double oscene_score(OEnv *e) {
     }
     return 0.0;
 }
+
+/* ---------------- reference control-flow fixtures ------------------------
+ * tests/golden/make_ref_fixtures.py executes the reference's OWN reset code (task on_reset, geom.py
+ * pm_randomise_all_poses / pm_randomise_pose / pm_shift_bodies) over a stand-in pymunk Space whose
+ * entities, poses, shape filters and shape queries are these: the entity builders and the collision test
+ * of this oracle, driven in the order the reference code calls them.  TEST INFRASTRUCTURE ONLY. */
+OEnv *osc_create(int task, int flags) {
+    OEnv *e = (OEnv *)calloc(1, sizeof(OEnv));
+    e->task = task; e->flags = flags; e->max_tries = 10000;
+    e->robot = -1; e->goal = -1;
+    ophys_init(&e->space);
+    static const double PV_DEF[5] = {3, 1, 4, 1.5, 0.1};
+    for (int i = 0; i < 5; i++) e->pv[i] = PV_DEF[i];  /* joint forces only: no effect on poses at reset */
+    return e;
+}
+void osc_destroy(OEnv *e) { free(e); }
+int osc_add_arena(OEnv *e) { add_arena(e); return e->nents - 1; }
+int osc_add_goal(OEnv *e, double x, double y, double h, double w, int colour) {
+    add_goal(e, x, y, h, w, colour); return e->nents - 1;
+}
+int osc_add_robot(OEnv *e, double x, double y, double angle) { add_robot(e, v2(x, y), angle); return e->nents - 1; }
+int osc_add_block(OEnv *e, int type, int colour, double x, double y, double angle) {
+    add_block(e, type, colour, v2(x, y), angle, 0); return e->nents - 1;
+}
+/* kind, body0, nbodies (goal: 1, its static body), shape0, nshapes */
+void osc_entity(const OEnv *e, int ent, int out[5]) {
+    const OEntity *en = &e->ents[ent];
+    out[0] = en->kind; out[1] = en->body0; out[2] = en->kind == ENT_GOAL ? 1 : en->nbodies;
+    out[3] = en->shape0; out[4] = en->nshapes;
+}
+/* pose of the k-th body of an entity (the goal's static body: its shape's static position, angle 0) */
+void osc_get_pose(OEnv *e, int ent, int k, double out[3]) {
+    const OEntity *en = &e->ents[ent];
+    if (en->kind == ENT_GOAL) { vec2 p = e->space.shapes[en->shape0].sp; out[0] = p.x; out[1] = p.y; out[2] = 0.0; return; }
+    const OBody *b = &e->space.bodies[en->body0 + k];
+    out[0] = b->p.x; out[1] = b->p.y; out[2] = b->a;
+}
+/* pymunk Body.position / Body.angle setters (cpBodySetPosition / cpBodySetAngle) */
+void osc_set_position(OEnv *e, int ent, int k, double x, double y) {
+    const OEntity *en = &e->ents[ent];
+    if (en->kind == ENT_GOAL) { e->space.shapes[en->shape0].sp = v2(x, y); return; }
+    ophys_body_set_position(&e->space, en->body0 + k, v2(x, y));
+}
+void osc_set_angle(OEnv *e, int ent, int k, double a) {
+    const OEntity *en = &e->ents[ent];
+    if (en->kind == ENT_GOAL) return;   /* static goal body: rand_rot is always False for it */
+    ophys_body_set_angle(&e->space, en->body0 + k, a);
+}
+/* Space.reindex_shapes_for_body of every body of the entity */
+void osc_reindex(OEnv *e, int ent) { reindex_entity(e, &e->ents[ent]); }
+void osc_get_filter(const OEnv *e, int sh, uint32_t out[3]) {
+    const OShape *s = &e->space.shapes[sh];
+    out[0] = s->group; out[1] = s->categories; out[2] = s->mask;
+}
+void osc_set_filter(OEnv *e, int sh, uint32_t group, uint32_t categories, uint32_t mask) {
+    OShape *s = &e->space.shapes[sh];
+    s->group = group; s->categories = categories; s->mask = mask;
+}
+/* Space.shape_query(shape): the shapes that collide with it (each once, in shape order) */
+int osc_shape_query(OEnv *e, int sh, int *hits, int max) {
+    int n = 0;
+    uint8_t ign[O_MAX_SHAPES];
+    memset(ign, 0, sizeof(ign));
+    while (n < max && ophys_shape_query_any_ign(&e->space, sh, ign)) {
+        /* find the first hit not yet reported: query with every earlier hit ignored */
+        int found = -1;
+        for (int j = 0; j < e->space.nshapes && found < 0; j++) {
+            if (ign[j] || j == sh) continue;
+            uint8_t only[O_MAX_SHAPES];
+            for (int k = 0; k < e->space.nshapes; k++) only[k] = (k != j);
+            if (ophys_shape_query_any_ign(&e->space, sh, only)) found = j;
+        }
+        if (found < 0) break;
+        hits[n++] = found;
+        ign[found] = 1;
+    }
+    return n;
+}
+/* the env's numpy-legacy MT19937 state (RandomState.get_state()[1:3]) */
+void oenv_get_rng(const OEnv *e, uint32_t key[624], int *pos) {
+    memcpy(key, e->rng.key, sizeof(e->rng.key));
+    *pos = e->rng.pos;
+}
+/* body index of a shape (-1: a static body) */
+int osc_shape_body(const OEnv *e, int sh) { return e->space.shapes[sh].body; }

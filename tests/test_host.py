@@ -80,6 +80,91 @@ def test_header_and_binding_agree():
     assert _header_functions() == sorted(native.EXPORTS)
 
 
+_C_TO_CTYPES = {"int32_t": ctypes.c_int32, "uint32_t": ctypes.c_uint32, "int64_t": ctypes.c_int64,
+                "double": ctypes.c_double}
+
+
+def _header_structs():
+    """{struct name: [(field, ctypes type or 'ptr')]} of the header's typedef'd structs, in field order."""
+    src = open(os.path.join(ROOT, "include", "magical_sim.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    out = {}
+    for body, name in re.findall(r"typedef struct \{(.*?)\}\s*(\w+);", src, flags=re.S):
+        fields = []
+        for decl in body.split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            m = re.match(r"(?:const\s+)?(\w+)\s*(\*?)\s*(\w+)$", decl)
+            assert m, decl
+            fields.append((m.group(3), "ptr" if m.group(2) else _C_TO_CTYPES[m.group(1)]))
+        out[name] = fields
+    return out
+
+
+def _integration_stub():
+    """Execute INTEGRATION.md section 2's ctypes stub with a recorder in place of ctypes.CDLL."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = text[text.index("## 2."):text.index("## 3.")]
+    code = re.search(r"```python\n(.*?)```", sec, flags=re.S).group(1)
+
+    class Fn:
+        pass
+
+    class Lib:
+        def __getattr__(self, name):
+            f = Fn()
+            object.__setattr__(self, name, f)
+            return f
+
+    ns = {"__Lib": Lib, "__name__": "integration_stub"}
+    exec(compile(code.replace('ctypes.CDLL("magical_amd/libmagical_sim.so")', "__Lib()"), "INTEGRATION.md", "exec"),
+         ns)
+    return ns
+
+
+def _same_ctype(a, b):
+    if a is b:
+        return True
+    # POINTER(X) of two different Structure classes with the same layout
+    return (getattr(a, "_type_", None) is not None and getattr(b, "_type_", None) is not None and
+            issubclass(a, ctypes._Pointer) and issubclass(b, ctypes._Pointer) and
+            [f[0] for f in getattr(a._type_, "_fields_", [])] == [f[0] for f in getattr(b._type_, "_fields_", [])])
+
+
+def test_integration_stub_matches_binding_and_header():
+    """INTEGRATION.md's ctypes stub (what a reference maintainer would copy) declares the same struct fields,
+    in the same order with the same types, as magical_amd/native.py and include/magical_sim.h (a short
+    mg_buffers makes mg_bind_outputs read past the caller's struct), and the same argument lists for every
+    function it binds."""
+    ns = _integration_stub()
+    header = _header_structs()
+    for name in ("mg_config", "mg_buffers"):
+        stub = [(f, t) for f, t in ns[name]._fields_]
+        ours = [(f, t) for f, t in getattr(native, name)._fields_]
+        assert [f for f, _ in stub] == [f for f, _ in ours] == [f for f, _ in header[name]], name
+        for (f, ts), (_, to), (_, th) in zip(stub, ours, header[name]):
+            assert ts is to, (name, f)
+            if th == "ptr":
+                assert ts is ctypes.c_void_p or issubclass(ts, ctypes._Pointer), (name, f)
+            else:
+                assert ts is th, (name, f)
+        assert ctypes.sizeof(ns[name]) == ctypes.sizeof(getattr(native, name))
+    lib = native.load()
+    stub_lib = ns["lib"]
+    bound = [k for k in vars(stub_lib) if k.startswith("mg_")]
+    assert {"mg_create", "mg_bind_outputs", "mg_step", "mg_restack", "mg_replay_lores"} <= set(bound)
+    for fn in bound:
+        f = getattr(stub_lib, fn)
+        if hasattr(f, "argtypes"):
+            ref = getattr(lib, fn).argtypes
+            assert len(f.argtypes) == len(ref), fn
+            assert all(_same_ctype(a, b) for a, b in zip(f.argtypes, ref)), fn
+    # the check itself fails on a removed field
+    short = [f for f in ns["mg_buffers"]._fields_ if f[0] != "frames_only"]
+    assert [f for f, _ in short] != [f for f, _ in header["mg_buffers"]]
+
+
 def test_library_loads_and_exports_every_header_symbol():
     lib = native.load()
     for name in _header_functions():
@@ -268,17 +353,74 @@ env.close()
 dist.destroy_process_group()
 """
 
+def test_frames_gather_refuses_a_stale_ring():
+    """gather_mode 'frames' rebuilds stacks from the receivers' frame rings, which only reset_async()
+    fills -- step_async() raises before the shard's first reset_async() and after a direct reset of the
+    VecMagicalEnv underneath; CPU tensors default to gather_mode 'stacked' (no restacker needed); the ring holds
+    only the stacked outputs' views."""
+    import torch
+    import torch.distributed as tdist
+    name, n = "MoveToRegion-Demo-LoRes4E-v0", 2
+    spec = registry.lookup(name)
+
+    class FakeVec:
+        device = torch.device("cpu")
+        def __init__(self):
+            self.reset_count = 0
+        def bind_outputs(self, views, frames_only=False):
+            self.v = views
+        def reset(self):
+            self.reset_count += 1
+            for t in self.v.values():
+                t.zero_()
+        def step(self, actions):
+            pass
+        def close(self):
+            pass
+
+    restacked = []
+    stacker = lambda recv, outs, step, all_fresh: restacked.append((step, all_fresh))  # noqa: E731
+    assert mdist.ShardedVecEnv(name, n, rank=0, gather=True, vec=FakeVec(), device="cpu").gather_mode == "stacked"
+    env = mdist.ShardedVecEnv(name, n, rank=0, gather=True, vec=FakeVec(), device="cpu", restacker=stacker)
+    assert env.gather_mode == "frames"
+    with pytest.raises(RuntimeError, match="before the first step"):
+        env.step_async(torch.zeros(n, dtype=torch.uint8))
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        env.reset_async()
+        env.step_async(torch.zeros(n, dtype=torch.uint8))
+        env.vec.reset()
+        with pytest.raises(RuntimeError, match="reset directly"):
+            env.step_async(torch.zeros(n, dtype=torch.uint8))
+        env.reset_async()
+        env.step_async(torch.zeros(n, dtype=torch.uint8))
+        env.close()
+    finally:
+        tdist.destroy_process_group()
+    assert restacked == [(0, True), (1, False), (2, True), (3, False)]
+    fr = 96 * 96 * 3
+    assert mdist.restack_ring_bytes("LoRes4E", 8, 10) == 4 * 80 * fr
+    assert mdist.restack_ring_bytes("LoResStack", 8, 10) == 2 * 4 * 80 * fr
+    assert spec.preproc == "LoRes4E"
+
+
 def test_bench_launches_ranks_itself():
     """bench.py --gpus 2 without WORLD_SIZE re-runs itself under torch.distributed.run with 2 ranks
     (before any GPU call); --dry-run swaps the GPU work for a gloo all-reduce, so rank 0 sees 2 ranks and
     the N > 1 gather default is on."""
     import json
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                          "--cpu-steps", "60", "--cpu-workers", "2"],
                          capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 0, out.stderr[-2000:]
     line = json.loads(out.stdout.strip().splitlines()[-1])
     assert line["ranks_seen"] == 2 and line["n_gpus"] == 2 and line["gather"] is True
+    # the N > 1 line carries the CPU baseline, measured in the launcher parent before the ranks start
+    cpu = line["cpu_baseline"]
+    assert cpu["measured_in"] == "launcher parent" and cpu["cores"] == 2 and cpu["kind"] == "port"
+    assert cpu["value"] > 0 and cpu["one_core_env_steps_s"] > 0
 
 
 def test_bench_byte_models():
@@ -291,6 +433,19 @@ def test_bench_byte_models():
     assert bench.render_bytes("LoResStack") == 221184 + 8 * fr
     assert bench.render_bytes("LoRes4E", frames_only=True) == 2 * fr
     assert bench.restack_bytes("LoResStack") == 2 * 9 * fr
+    # roofline.frac: SURVEY 8(d) bytes per env-step (obs + ~2 KB state) for whichever kernel dominates
+    assert bench.survey_bytes("LoRes4E") == 167936 and bench.survey_bytes("LoResStack") == 223232
+    # MoveToRegion render at 4096 envs, rocprofv3 average 1.0484 ms (profiles/r03_final): 656 GB/s = 0.082
+    r = bench.kernel_record("render_kernel", 1.0484, "LoRes4E", 4096,
+                            {"bytes_per_launch": 1.272e9, "valu_issue_frac": 0.32, "wait_any_frac": 0.64})
+    assert abs(r["achieved_gbs"] - 656.1) < 0.5 and 0.082 <= r["hbm_frac"] <= 0.083
+    assert abs(r["traffic_ratio"] - 1.85) < 0.01            # 1.272 GB over 167 936 B x 4096
+    assert r["kernel_bytes_per_env_step"] == 165888 + 4 * fr  # the ring-inclusive figure, kept apart
+    # the step kernel's traffic ratio is over its 8(d) state bytes: ClusterColour's 4.37 GB at 8192 envs ~ 260x
+    s = bench.kernel_record("step_kernel", 3.82, "LoResStack", 8192, {"bytes_per_launch": 4.367e9})
+    assert s["bytes_per_env_step"] == 223232 and s["traffic_ratio_basis_bytes_per_env_step"] == 2048
+    assert 255 < s["traffic_ratio"] < 265
+    assert bench.kernel_record("step_kernel", 1.0, "LoRes4E", 64, None)["traffic_ratio"] is None
 
 
 GATHER_CASES = [("MoveToRegion-Demo-LoRes4E-v0", "frames"), ("MoveToRegion-Demo-LoRes4E-v0", "stacked"),
