@@ -231,6 +231,10 @@ def main():
     ap.add_argument("--no-phase-spread", action="store_true",
                     help="start every env at episode step 0 (resets then happen on the same step for all envs)")
     ap.add_argument("--dry-run", action="store_true", help="launcher / process-group check only (gloo, no GPU)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="one GPU runs rank 0 of a W-rank node's exchange: each step's frames-only buffer is copied "
+                         "into all W receive blocks (standing in for the all-gather) and restacked for W x envs on "
+                         "the restack stream, beside the next step (value stays this rank's env-steps/s x W)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -281,11 +285,12 @@ def main():
         dist.init_process_group("nccl", device_id=device)
     n = args.envs
     seeds = [1000 + rank * n + i for i in range(n)]
-    gather = (world > 1) if args.gather is None else (args.gather and world > 1)
+    emulate = args.emulate_world if world == 1 and args.emulate_world > 1 else 0
+    gather = (world > 1 or emulate > 0) if args.gather is None else (args.gather and (world > 1 or emulate > 0))
     if gather:
         from magical_amd import dist as mdist
         shard = mdist.ShardedVecEnv(args.env, n, rank=rank, device=str(device), gather=True,
-                                    gather_mode=args.gather_mode)
+                                    gather_mode=args.gather_mode, emulate_world=emulate or None)
         vec = shard.vec
         step = shard.step_async
     else:
@@ -308,6 +313,8 @@ def main():
         shard.wait_all()
     torch.cuda.synchronize(device)
     native.check(lib.mg_enable_timing(vec.handle, args.steps))
+    if gather:
+        shard.enable_restack_timing()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
@@ -335,7 +342,8 @@ def main():
         e = torch.tensor([errors, 1], dtype=torch.int64, device=device)
         dist.all_reduce(e)
         errors, ranks_seen = int(e[0].item()), int(e[1].item())
-    value = world * n * args.steps / elapsed
+    value = world * n * args.steps / elapsed   # (--emulate-world: this rank's env-steps/s under the W-rank load)
+    restack_ms = shard.restack_ms() / args.steps if gather and shard.restack_timing else None
     if rank == 0:
         frames_only = gather and args.gather_mode == "frames"
         kernels = {
@@ -351,6 +359,7 @@ def main():
             "value": round(value, 1),
             "unit": "env-steps/s",
             "n_gpus": world,
+            "emulated_world": emulate or None,
             "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -385,10 +394,13 @@ def main():
             "kernel_ms_per_step": {"step_kernel": round(t_step_ms, 4), "reset_kernel": round(t_reset_ms, 4),
                                    "render_kernel": round(t_render_ms, 4), "timed_launches": n_timed},
             "env_errors": errors,
-            "gather": ({"mode": args.gather_mode, "ranks": world, "bytes_per_rank_step": shard.layout.nbytes,
+            "gather": ({"mode": args.gather_mode, "ranks": shard.world, "bytes_per_rank_step": shard.layout.nbytes,
                         "stacked_bytes_per_rank_step": shard.stacked_nbytes,
-                        "received_bytes_per_rank_step": (world - 1) * shard.layout.nbytes,
-                        "restack_bytes_per_rank_step": (world * n * restack_bytes(spec.preproc) if frames_only else 0)}
+                        "received_bytes_per_rank_step": (shard.world - 1) * shard.layout.nbytes,
+                        "restack_bytes_per_rank_step": (shard.world * n * restack_bytes(spec.preproc)
+                                                        if frames_only else 0),
+                        "emulated": bool(emulate),
+                        "restack_ms_per_step": round(restack_ms, 4) if restack_ms is not None else None}
                        if gather else None),
             "cpu_baseline": cpu,
         }

@@ -1,6 +1,7 @@
-// mg_physics.hip -- step-kernel dispatch: the compiled form for a scene's slot caps (variants
-// 1/2: compile-time constraint lists, 3/4: LDS views with runtime lists, 0: HBM state) and envs per
-// workgroup.  The forms themselves live in mg_step_*.hip (one translation unit each).
+// mg_physics.hip -- step-kernel dispatch: the compiled form for a scene's slot caps (5/6: compile-time
+// constraint lists with 4 lanes per env, 4: cooperative LDS view with runtime lists, one env per wavefront,
+// 0: HBM state for scenes beyond the LDS caps) and envs per workgroup.  The forms live in mg_step_*.hip (one
+// translation unit each); the superseded one-lane forms 1/2/3 only in comparison builds (MG_ALL_STEP_FORMS).
 #include "mg_launch.h"
 #include "mg_phys.h"   // sizeof(ShapeW) of the LDS views
 
@@ -42,10 +43,14 @@ int mg_step_variant(const StepCaps &c, int n_envs) {
 
 // envs per workgroup: compiled sizes only
 bool mg_step_blk_ok(int variant, int blk) {
+#ifndef MG_ALL_STEP_FORMS
+    if (variant >= 1 && variant <= 3) return false;
+#endif
     return variant == 0 ? (blk == 1 || blk == 8 || blk == 64)
          : variant == 3 ? (blk == 1 || blk == 4)
          : variant == 4 ? blk == 1
-         : variant == 5 || variant == 6 ? (blk == 4 || blk == 8 || blk == 16)
+         : variant == 5 ? (blk == 4 || blk == 8 || blk == 16)
+         : variant == 6 ? blk == 16   // (6 / 8 faulted on the GPU in round 4: not compiled)
          : (blk == 1 || blk == 4 || blk == 16);
 }
 
@@ -55,10 +60,13 @@ hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, in
 #define MG_STEP_CASE(V, B) \
     if (variant == V && blk == B) \
         return launch_step_var<V, B>(S, L, cfg, max_steps, auto_reset, actions, reward, done, eval_score, reset_mask, st);
+#ifdef MG_ALL_STEP_FORMS   // comparison builds only (build.py --all-forms): the superseded one-lane forms
     MG_STEP_CASE(1, 1) MG_STEP_CASE(1, 4) MG_STEP_CASE(1, 16)
     MG_STEP_CASE(2, 1) MG_STEP_CASE(2, 4) MG_STEP_CASE(2, 16)
-    MG_STEP_CASE(3, 1) MG_STEP_CASE(3, 4) MG_STEP_CASE(4, 1)
-    MG_STEP_CASE(5, 16) MG_STEP_CASE(6, 16) MG_STEP_CASE(5, 8) MG_STEP_CASE(6, 8) MG_STEP_CASE(5, 4) MG_STEP_CASE(6, 4)
+    MG_STEP_CASE(3, 1) MG_STEP_CASE(3, 4)
+#endif
+    MG_STEP_CASE(4, 1)
+    MG_STEP_CASE(5, 16) MG_STEP_CASE(6, 16) MG_STEP_CASE(5, 8) MG_STEP_CASE(5, 4)
     MG_STEP_CASE(0, 1) MG_STEP_CASE(0, 8) MG_STEP_CASE(0, 64)
 #undef MG_STEP_CASE
     return hipErrorInvalidValue;
@@ -67,8 +75,10 @@ hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, in
 hipError_t mg_prof_read_physics(unsigned long long *out) {
     hipError_t e;
     if ((e = mg_prof_read_reset(out)) != hipSuccess) return e;
+#ifdef MG_ALL_STEP_FORMS
     if ((e = mg_prof_read_step_robot(out)) != hipSuccess) return e;
     if ((e = mg_prof_read_step_v3(out)) != hipSuccess) return e;
+#endif
     if ((e = mg_prof_read_step_v4(out)) != hipSuccess) return e;
     if ((e = mg_prof_read_step_quad(out)) != hipSuccess) return e;
     return mg_prof_read_step_hbm(out);

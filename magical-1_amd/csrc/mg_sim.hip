@@ -262,9 +262,10 @@ static int pick_step_variant(const StepCaps &c, int n_envs, int task) {
     if (v == 3) v = 4;
     if (v == 1 || v == 2) v += 4;
     const char *ov = getenv("MG_STEP_VARIANT");
-    if (ov) { // experiments: 0 (HBM state), the scene's compiled variant (1 / 2, or 5 / 6), 3 / 4 (LDS runtime lists)
+    if (ov) { // experiments: 0 (HBM state), the scene's compiled variant (5 / 6; 1 / 2 in comparison builds),
+              // 3 / 4 (LDS runtime lists)
         const int w = atoi(ov), base = mg_step_variant(c, n_envs);
-        if (w == 0 || w == base || w == 3 || w == 4) v = w;   // 3 / 4 fit every scene (caps 14/53/26/48)
+        if (w == 0 || ((w == base || w == 3) && mg_step_blk_ok(w, w == 3 ? 1 : 16)) || w == 4) v = w;
         if ((base == 1 || base == 2) && w == base + 4) v = w;  // 5 / 6: the compiled lists, 4 lanes per env
     }
     return v;

@@ -221,10 +221,18 @@ class ShardedVecEnv:
     reset directly (vec.reset()), since the other ranks' rings would then hold stale frames of its envs."""
 
     def __init__(self, env_name, envs_per_rank, rank=None, device=None, base_seed=1000, gather=False, vec=None,
-                 gather_mode=None, restacker=None, max_episode_steps=None):
+                 gather_mode=None, restacker=None, max_episode_steps=None, emulate_world=None):
         from . import registry
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if dist.is_initialized() else 1
+        # measurement only (bench.py --emulate-world W): one process stands in for rank 0 of a W-rank node --
+        # the all-gather is replaced by a device copy of this rank's buffer into all W receive blocks (the
+        # HBM writes a real all-gather makes on the receiver), and the restack rebuilds W * n envs' stacks
+        self.emulate_world = None
+        if emulate_world and emulate_world > 1:
+            if self.world != 1:
+                raise ValueError("emulate_world is a single-process measurement mode")
+            self.emulate_world = self.world = int(emulate_world)
         self.envs_per_rank = envs_per_rank
         self.gather = gather
         spec = registry.lookup(env_name)
@@ -264,6 +272,21 @@ class ShardedVecEnv:
             self.restacked = [None, None]   # per buffer set: event after the restack that last read recv[b]
             self.t = 0
             self._ring_resets = None        # vec.reset_count at the last reset_async (frames mode: ring valid)
+            self.restack_timing = False
+            self._restack_ev = []
+
+    def enable_restack_timing(self):
+        """time every following restack with HIP events on the restack stream (bench.py)"""
+        self.restack_timing = self.restack_stream is not None
+        self._restack_ev = []
+
+    def restack_ms(self):
+        """total ms of the restacks timed since enable_restack_timing (synchronises on the last one)"""
+        tot = 0.0
+        for a, b in self._restack_ev:
+            b.synchronize()
+            tot += a.elapsed_time(b)
+        return tot
 
     # -- packed gather pipeline ---------------------------------------------------------------------------
     def _begin(self):
@@ -290,14 +313,24 @@ class ShardedVecEnv:
                 self.comm_stream.wait_event(ev)
                 if self.restacked[b] is not None:   # the restack of step t - 2 has read recv[b]
                     self.comm_stream.wait_event(self.restacked[b])
-                work = dist.all_gather_into_tensor(recv, send, async_op=True)
-                work.wait()   # the side stream (not the host) waits for the collective
+                if self.emulate_world:
+                    recv.view(self.world, -1).copy_(send.unsqueeze(0).expand(self.world, -1))
+                else:
+                    work = dist.all_gather_into_tensor(recv, send, async_op=True)
+                    work.wait()   # the side stream (not the host) waits for the collective
                 done_ev = self.comm_stream.record_event()
             if stacks is not None:
                 # in step order on its own stream (the receive ring carries state from step to step)
                 with torch.cuda.stream(self.restack_stream):
                     self.restack_stream.wait_event(done_ev)
+                    if self.restack_timing:
+                        t0 = torch.cuda.Event(enable_timing=True)
+                        t0.record(self.restack_stream)
                     self.restacker(recv, stacks, step, all_fresh)
+                    if self.restack_timing:
+                        t1 = torch.cuda.Event(enable_timing=True)
+                        t1.record(self.restack_stream)
+                        self._restack_ev.append((t0, t1))
                     done_ev = self.restacked[b] = self.restack_stream.record_event()
             h = GatheredStep(self.layout, recv, stacks, event=done_ev)
         else:

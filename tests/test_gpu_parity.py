@@ -115,31 +115,21 @@ def test_rollout_parity(name, n, steps):
 
 
 # every compiled step-kernel (and render-class) form, forced through the experiment switches read at mg_create
-# (MG_STEP_VARIANT: 0 = HBM state, 1/2 = compile-time constraint lists with one env per lane, 5/6 (default
-# for those scenes) = the same with 4 lanes per env, 3 = LDS with runtime lists and one env per single-lane
-# workgroup, 4 (default for those scenes) = the same one env per 64-lane wavefront; MG_STEP_BLK /
-# MG_STEP_BLK0: envs per workgroup)
+# (MG_STEP_VARIANT: 0 = HBM state (the default for scenes beyond the LDS caps), 5/6 = compile-time
+# constraint lists with 4 lanes per env (robot scenes), 4 = LDS with runtime lists, one env per 64-lane
+# wavefront (every other scene); MG_STEP_BLK / MG_STEP_BLK0: envs per workgroup.  The superseded one-lane
+# forms 1/2/3 are only in comparison builds, magical_amd.build --all-forms)
 KERNEL_FORMS = [
-    ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "1", "MG_STEP_BLK": "1"}),
-    ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "1", "MG_STEP_BLK": "4"}),
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "8"}),
-    ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "2", "MG_STEP_BLK": "4"}),
     # 4 lanes per env (16 envs per 64-lane workgroup; 70 envs leave shadow lanes in the last one)
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5"}),
     ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "6"}),
     # the same with 8 / 4 envs per workgroup (8 / 16 lanes per env)
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5", "MG_STEP_BLK": "8"}),
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5", "MG_STEP_BLK": "4"}),
-    ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "6", "MG_STEP_BLK": "8"}),
-    ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "6", "MG_STEP_BLK": "4"}),
-    ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "1"}),
-    ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "2"}),
     ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "1"}),
-    ("ClusterColour-Demo-LoResStack-v0", 66, 30, {"MG_STEP_VARIANT": "3", "MG_STEP_BLK": "1"}),
-    ("ClusterColour-Demo-LoResStack-v0", 66, 30, {"MG_STEP_VARIANT": "3", "MG_STEP_BLK": "4"}),
     ("ClusterColour-Demo-LoResStack-v0", 66, 30, {"MG_STEP_VARIANT": "4"}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "4"}),
-    ("FindDupe-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "3"}),
     ("ClusterShape-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0"}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0"}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "8"}),
