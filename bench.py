@@ -399,7 +399,7 @@ def main():
                         "received_bytes_per_rank_step": (shard.world - 1) * shard.layout.nbytes,
                         "restack_bytes_per_rank_step": (shard.world * n * restack_bytes(spec.preproc)
                                                         if frames_only else 0),
-                        "emulated": bool(emulate),
+                        "emulated": bool(emulate), "emulated_copy": shard.emulated_copy,
                         "restack_ms_per_step": round(restack_ms, 4) if restack_ms is not None else None}
                        if gather else None),
             "cpu_baseline": cpu,

@@ -351,20 +351,18 @@ MG_COLLIDE_ATTR bool collide(const ShapeW &A, const ShapeW &B, Collision &info) 
             V2 n = info.n = (dist != 0.0 ? vmult(delta, 1.0 / dist) : b.n);
             push_contact(info, vadd(a.c, vmult(n, a.r)), vadd(closest, vmult(n, -b.r)), 0);
         }
-    } else if (code == 6) { // circle-poly
+    } else if (code >= 6) { // circle-poly (6), segment-poly (7), poly-poly (8): one GJK / EPA for the three,
+                            // so the narrowphase inlines it once
         Closest pts = gjk(a, b);
-        if (pts.d <= a.r + b.r) {
-            V2 n = info.n = pts.n;
-            push_contact(info, vadd(pts.a, vmult(n, a.r)), vadd(pts.b, vmult(n, -b.r)), 0);
+        if (code == 6) {
+            if (pts.d <= a.r + b.r) {
+                V2 n = info.n = pts.n;
+                push_contact(info, vadd(pts.a, vmult(n, a.r)), vadd(pts.b, vmult(n, -b.r)), 0);
+            }
+        } else if (pts.d - a.r - b.r <= 0.0) {
+            const Edge ea = code == 7 ? support_edge_segment(a, pts.n) : support_edge_poly(a, pts.n);
+            contact_points(ea, support_edge_poly(b, vneg(pts.n)), pts, info);
         }
-    } else if (code == 7) { // segment-poly
-        Closest pts = gjk(a, b);
-        if (pts.d - a.r - b.r <= 0.0)
-            contact_points(support_edge_segment(a, pts.n), support_edge_poly(b, vneg(pts.n)), pts, info);
-    } else if (code == 8) { // poly-poly
-        Closest pts = gjk(a, b);
-        if (pts.d - a.r - b.r <= 0.0)
-            contact_points(support_edge_poly(a, pts.n), support_edge_poly(b, vneg(pts.n)), pts, info);
     }
     return sw;
 }

@@ -49,8 +49,7 @@ bool mg_step_blk_ok(int variant, int blk) {
     return variant == 0 ? (blk == 1 || blk == 8 || blk == 64)
          : variant == 3 ? (blk == 1 || blk == 4)
          : variant == 4 ? blk == 1
-         : variant == 5 ? (blk == 4 || blk == 8 || blk == 16)
-         : variant == 6 ? blk == 16   // (6 / 8 faulted on the GPU in round 4: not compiled)
+         : variant == 5 || variant == 6 ? blk == 16   // 8 / 4 envs per workgroup measured slower (round 4)
          : (blk == 1 || blk == 4 || blk == 16);
 }
 
@@ -66,7 +65,7 @@ hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, in
     MG_STEP_CASE(3, 1) MG_STEP_CASE(3, 4)
 #endif
     MG_STEP_CASE(4, 1)
-    MG_STEP_CASE(5, 16) MG_STEP_CASE(6, 16) MG_STEP_CASE(5, 8) MG_STEP_CASE(5, 4)
+    MG_STEP_CASE(5, 16) MG_STEP_CASE(6, 16)
     MG_STEP_CASE(0, 1) MG_STEP_CASE(0, 8) MG_STEP_CASE(0, 64)
 #undef MG_STEP_CASE
     return hipErrorInvalidValue;

@@ -8,6 +8,7 @@
 // both HBM-bound byte work: (1) every frame's two views downsampled once into a workspace, (2) each
 // frame's outputs assembled from the workspace frames its stacks reach back to (clamped to the first
 // frame of its trajectory).
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "mg_common.h"
@@ -128,48 +129,49 @@ __global__ __launch_bounds__(256) void restack_kernel(const uint8_t *__restrict_
                                                       uint8_t *__restrict__ out1) {
     constexpr uint32_t Q = LO * LO / 4;
     const uint32_t W = world * n;
-    const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t g = gid / Q, q = gid - g * Q;
-    if (g >= W) return;
     const int s = blockIdx.y;
-    const uint32_t r = g / n, i = g - r * n;
-    const uint8_t *blk = recv + (size_t)r * stride;
-    const bool fresh = all_fresh || blk[off_d + i] != 0;
-    // the view this stack's frames come from (LoRes3EA: ego, with the current allo frame in slot 0)
-    const int rv = (preproc == MG_PREPROC_LORES4A || (preproc == MG_PREPROC_LORESSTACK && s == 0)) ? 0 : 1;
-    const size_t po = (size_t)q * 12;
-    const uint32_t *cur = (const uint32_t *)(blk + (rv ? off_e : off_a) + (size_t)i * LOFR + po);
-    uint8_t *rring = ring + (size_t)s * 4 * W * LOFR;   // one ring per output stack (LoResStack: 2, else 1)
-    auto rslot = [&](uint32_t sl) { return (uint32_t *)(rring + ((size_t)(sl & 3) * W + g) * LOFR + po); };
-    uint32_t f[4][3];
+    // grid-stride (a capped grid leaves the SIMDs' register files to the simulator's kernels, MG_RESTACK_WGS)
+    for (uint32_t gid = blockIdx.x * 256u + threadIdx.x; gid < W * Q; gid += gridDim.x * 256u) {
+        const uint32_t g = gid / Q, q = gid - g * Q;
+        const uint32_t r = g / n, i = g - r * n;
+        const uint8_t *blk = recv + (size_t)r * stride;
+        const bool fresh = all_fresh || blk[off_d + i] != 0;
+        // the view this stack's frames come from (LoRes3EA: ego, with the current allo frame in slot 0)
+        const int rv = (preproc == MG_PREPROC_LORES4A || (preproc == MG_PREPROC_LORESSTACK && s == 0)) ? 0 : 1;
+        const size_t po = (size_t)q * 12;
+        const uint32_t *cur = (const uint32_t *)(blk + (rv ? off_e : off_a) + (size_t)i * LOFR + po);
+        uint8_t *rring = ring + (size_t)s * 4 * W * LOFR;   // one ring per output stack (LoResStack: 2, else 1)
+        auto rslot = [&](uint32_t sl) { return (uint32_t *)(rring + ((size_t)(sl & 3) * W + g) * LOFR + po); };
+        uint32_t f[4][3];
 #pragma unroll
-    for (int w = 0; w < 3; w++) f[3][w] = cur[w];
-    if (fresh) {
+        for (int w = 0; w < 3; w++) f[3][w] = cur[w];
+        if (fresh) {
 #pragma unroll
-        for (int k = 0; k < 3; k++)
+            for (int k = 0; k < 3; k++)
 #pragma unroll
-            for (int w = 0; w < 3; w++) f[k][w] = f[3][w];
+                for (int w = 0; w < 3; w++) f[k][w] = f[3][w];
 #pragma unroll
-        for (uint32_t sl = 0; sl < 4; sl++) {
-            uint32_t *d = rslot(sl);
+            for (uint32_t sl = 0; sl < 4; sl++) {
+                uint32_t *d = rslot(sl);
+                d[0] = f[3][0]; d[1] = f[3][1]; d[2] = f[3][2];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; k++) {          // stack slot k = frame t - (3 - k)
+                const uint32_t *src = rslot(slot + 1 + k);
+#pragma unroll
+                for (int w = 0; w < 3; w++) f[k][w] = src[w];
+            }
+            uint32_t *d = rslot(slot);
             d[0] = f[3][0]; d[1] = f[3][1]; d[2] = f[3][2];
         }
-    } else {
+        if (preproc == MG_PREPROC_LORES3EA) {      // allo depth 1 in front of the ego frames t-2, t-1, t
+            const uint32_t *a = (const uint32_t *)(blk + off_a + (size_t)i * LOFR + po);
 #pragma unroll
-        for (int k = 0; k < 3; k++) {          // stack slot k = frame t - (3 - k)
-            const uint32_t *src = rslot(slot + 1 + k);
-#pragma unroll
-            for (int w = 0; w < 3; w++) f[k][w] = src[w];
+            for (int w = 0; w < 3; w++) f[0][w] = a[w];
         }
-        uint32_t *d = rslot(slot);
-        d[0] = f[3][0]; d[1] = f[3][1]; d[2] = f[3][2];
+        stack_regs(f, (s ? out1 : out0) + (size_t)g * LOFR * 4 + po * 4);
     }
-    if (preproc == MG_PREPROC_LORES3EA) {      // allo depth 1 in front of the ego frames t-2, t-1, t
-        const uint32_t *a = (const uint32_t *)(blk + off_a + (size_t)i * LOFR + po);
-#pragma unroll
-        for (int w = 0; w < 3; w++) f[0][w] = a[w];
-    }
-    stack_regs(f, (s ? out1 : out0) + (size_t)g * LOFR * 4 + po * 4);
 }
 }  // namespace
 
@@ -195,7 +197,10 @@ extern "C" hipError_t mg_launch_restack(const uint8_t *recv, int32_t world, int3
                                         hipStream_t st) {
     const int64_t t = (int64_t)world * n * (LO * LO / 4);
     const bool two = preproc == MG_PREPROC_LORESSTACK;
-    hipLaunchKernelGGL(restack_kernel, dim3((unsigned)((t + 255) / 256), two ? 2 : 1), dim3(256), 0, st, recv,
+    int64_t wgs = (t + 255) / 256;
+    static const int64_t cap = getenv("MG_RESTACK_WGS") ? atoll(getenv("MG_RESTACK_WGS")) : 0;   // experiments
+    if (cap > 0 && wgs > cap) wgs = cap;
+    hipLaunchKernelGGL(restack_kernel, dim3((unsigned)wgs, two ? 2 : 1), dim3(256), 0, st, recv,
                        (uint32_t)world, (uint32_t)n, stride, off_a, off_e, off_d, preproc, (uint32_t)(step & 3),
                        all_fresh, ring, two ? out_allo : out_past, out_ego);
     return hipGetLastError();

@@ -1493,8 +1493,11 @@ MG_DEV void robot_set_action(const MGState &S, const mg_library *L, int e, int a
     S.target_finger[e] = action < 9 ? L->finger_angle_off[0] : -0.0; // OPEN: pi/8, CLOSE: -finger_rot_limit_inner
 }
 
+// STATIC: the compile-time scenes (step forms 5 / 6: robot bodies at slots 0-5, its joints at 0-9, checked by
+// the step kernel) -- constant slots, no dependent LDS reads before the first access
+template <bool STATIC = false>
 MG_DEV void robot_update(const MGState &S, const mg_library *L, int e) {
-    int body = S.robot_body0[e], control = body + 1, cons0 = S.robot_cons0[e];
+    const int body = STATIC ? 0 : S.robot_body0[e], control = body + 1, cons0 = STATIC ? 0 : S.robot_cons0[e];
     AT(S.ba, control) = AT(S.ba, body) + S.rel_turn[e]; // transform unused (body_rot_unused)
     double c = AT(S.brc, body), s = AT(S.brs, body), ts = S.target_speed[e];
     AT(S.bvx, control) = c * 0.0 - s * ts;

@@ -4,9 +4,4 @@
 
 template hipError_t launch_step_var<5, 16>(const MGState &, const mg_library *, TaskCfg, int, int, const uint8_t *, float *, uint8_t *, double *, uint8_t *, hipStream_t);
 template hipError_t launch_step_var<6, 16>(const MGState &, const mg_library *, TaskCfg, int, int, const uint8_t *, float *, uint8_t *, double *, uint8_t *, hipStream_t);
-// 8 / 4 envs per 64-lane workgroup (8 / 16 lanes per env): more workgroups per CU, more lanes for the
-// order-free phases (MG_STEP_BLK)
-template hipError_t launch_step_var<5, 8>(const MGState &, const mg_library *, TaskCfg, int, int, const uint8_t *, float *, uint8_t *, double *, uint8_t *, hipStream_t);
-template hipError_t launch_step_var<5, 4>(const MGState &, const mg_library *, TaskCfg, int, int, const uint8_t *, float *, uint8_t *, double *, uint8_t *, hipStream_t);
-
 MG_PROF_READER(mg_prof_read_step_quad)

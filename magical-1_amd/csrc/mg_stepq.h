@@ -3,10 +3,11 @@
 // The forms 1 / 2 run one env per lane, 16 envs in a 16-lane wave per CU: every phase of an env's
 // substep is one lane's serial chain.  Here each env owns QL = 64 / BLK lanes of the workgroup's one
 // wavefront (16 envs x 4 lanes) and the order-free phases are split over them:
-//   * position integration and rotation caches (body b on lane b mod QL; the correctly rounded sincos of
-//     the robot body and fingers run side by side), cached shape BBs (shape k on lane k mod QL);
-//   * broadphase + narrowphase: shape i's candidate list (walls 0..3, then shapes j > i) in chunks of QL,
-//     candidate c on lane c mod QL (BB test, filters, exact skip, world shapes, collide);
+//   * position integration and rotation caches (quad_body: the robot body, fingers and block -- the bodies
+//     that need the correctly rounded sincos -- one per lane, side by side), cached shape BBs (shape k on
+//     lane k mod QL);
+//   * broadphase + narrowphase: the candidate list (shape i's walls 0..3, then shapes j > i) tested QL at a
+//     time into a mask of hits, then the hits QL at a time (world shapes, collide);
 //   * the stale-arbiter filter (slot on lane slot mod QL), arbiter pre-steps (active entry on lane
 //     entry mod QL) and the non-spring constraint pre-steps (constraint C on lane C mod QL).
 // The order-dependent parts stay on the env's lane 0 in the reference order: the arbiter updates (slot
@@ -41,50 +42,102 @@ MG_DEV void static_prestep_quad(const MGState &S, int e, int sub, double dt) {
     }
 }
 
+// body of integration slot p (p < nb) in the compile-time scenes (robot: body 0, control 1, eyes 2-3, fingers
+// 4-5; block 6): the bodies whose rotation caches need the correctly rounded sincos (0, 4, 5, 6) first, so the
+// first round of slots (one per lane) runs them side by side and the second has none (body_rot_unused)
+MG_DEV int quad_body(int p, int nb) {
+    if (p == 0) return 0;
+    if (p == 1) return 4;
+    if (p == 2) return 5;
+    if (nb == 7) return p == 3 ? 6 : p - 3;
+    return p - 2;
+}
+
+MG_DEV uint64_t qshfl_xor_u64(uint64_t u, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)u, m, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(u >> 32), m, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// candidate k of shape i in the canonical order (walls 0..3, then shapes j = i + 1 + (k - 4)): the broadphase
+// tests that decide whether collide() runs -- cached BBs, shape filters (categories 0: MG_GROUP_OFF), same
+// body / same group, and the exact separating-axis skip
+MG_DEV bool quad_candidate(const MGState &S, const mg_library *L, int e, int i, int k) {
+    const double al = AT(S.sbbl, i), ab = AT(S.sbbb, i), ar = AT(S.sbbr, i), at = AT(S.sbbt, i);
+    const int gi = AT(S.sgroup, i);
+    if (k < 4) {
+        if (gi & MG_GROUP_OFF) return false;   // categories 0 collide with nothing
+        double wl, wb, wr, wt;
+        wall_bb(k, wl, wb, wr, wt);
+        return al <= wr && wl <= ar && ab <= wt && wb <= at;
+    }
+    const int j = i + 1 + (k - 4), gj = AT(S.sgroup, j);
+    return al <= AT(S.sbbr, j) && AT(S.sbbl, j) <= ar && ab <= AT(S.sbbt, j) && AT(S.sbbb, j) <= at &&
+           AT(S.sbody, j) != AT(S.sbody, i) && !((gi != 0 && gi == gj) || ((gi | gj) & MG_GROUP_OFF)) &&
+           !surely_apart(S, L, e, i, j);
+}
+
 // broadphase + narrowphase of env e (canonical pair order), QL lanes per env.  Called with every lane of
-// the env active (the trip counts depend on the env's shape count only).
+// the env active (the trip counts depend on the env's shape count and hits only).
+// Pass 1: the env's candidates (shape i's walls 0..3, then shapes j > i, for i = 0 .. ns-1) are tested QL at
+// a time (candidate c on lane c mod QL) and the ones that need collide() form a mask in canonical order.  In
+// most substeps it is empty (the robot scenes touch a wall or the block now and then).  Pass 2: the hits, QL
+// at a time in mask order (the q-th lowest on lane q): collide(), then lane 0 applies the arbiter updates in
+// canonical order from its siblings' results (cross-lane reads).  The same collide() calls and the same
+// arbiter updates in the same order as a serial sweep of the candidates, so bit-identical.
 template <int NCS, int QL, bool LDS_SHAPES>
 MG_DEV void narrowphase_quad(const MGState &S, const mg_library *L, int e, int sub, int ns) {
     ShapeW locA, locB;
     ShapeW &A = LDS_SHAPES ? S.shw[2 * QL * e + 2 * sub] : locA;
     ShapeW &B = LDS_SHAPES ? S.shw[2 * QL * e + 2 * sub + 1] : locB;
     const int base = (int)(threadIdx.x & 63) - sub;   // the env's lane 0
-    for (int i = 0; i < ns; i++) {
-        const double al = AT(S.sbbl, i), ab = AT(S.sbbb, i), ar = AT(S.sbbr, i), at = AT(S.sbbt, i);
-        const int gi = AT(S.sgroup, i), bi = AT(S.sbody, i);
-        const double ui = AT(S.su, i);
-        const int ta = AT(S.spoly, i) < 0 ? WS_CIRCLE : WS_POLY;
-        const int ncand = 4 + ns - i - 1;   // walls 0..3, then shapes i+1 .. ns-1
-        for (int c0 = 0; c0 < ncand; c0 += QL) {
-            const int c = c0 + sub;
+    const int ntot = 4 * ns + (ns * (ns - 1)) / 2;
+    for (int w0 = 0; w0 < ntot; w0 += 64) {
+        const int wn = ntot - w0 < 64 ? ntot - w0 : 64;
+        uint64_t hits = 0;
+        {   // pass 1 (decode c -> (i, k) incrementally: candidates of one lane are QL apart)
+            int i = 0, k = w0 + sub;
+            while (i < ns && k >= 4 + ns - 1 - i) { k -= 4 + ns - 1 - i; i++; }
+            for (int c = sub; c < wn; c += QL) {
+                if (quad_candidate(S, L, e, i, k)) hits |= 1ull << c;
+                k += QL;
+                while (i < ns && k >= 4 + ns - 1 - i) { k -= 4 + ns - 1 - i; i++; }
+            }
+        }
+#pragma unroll
+        for (int off = 1; off < QL; off <<= 1) hits |= qshfl_xor_u64(hits, off);   // the env's lanes: disjoint bits
+        // pass 2
+        while (hits) {   // uniform over the env's lanes
+            uint64_t rest = hits;
+            int mine = -1;
+#pragma unroll
+            for (int q = 0; q < QL; q++) {
+                if (!rest) break;
+                const int b = __ffsll((long long)rest) - 1;
+                rest &= rest - 1;
+                if (q == sub) mine = b;
+            }
+            hits = rest;
             Collision info;
             info.count = 0;
-            int key = 0, tb = 0, bb = -1;
-            double ub = 0.0;
-            if (c < 4) {
-                if (!(gi & MG_GROUP_OFF)) {   // categories 0 collide with nothing
-                    double wl, wb, wr, wt;
-                    wall_bb(c, wl, wb, wr, wt);
-                    if (al <= wr && wl <= ar && ab <= wt && wb <= at) {
-                        load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A);
-                        load_wall(c, B);
-                        collide(A, B, info);
-                        key = i * 128 + 100 + c; ub = 0.8; tb = WS_SEGMENT; bb = -1;
-                    }
-                }
-            } else if (c < ncand) {
-                const int j = i + 1 + (c - 4);
-                const int gj = AT(S.sgroup, j);
-                if (al <= AT(S.sbbr, j) && AT(S.sbbl, j) <= ar && ab <= AT(S.sbbt, j) && AT(S.sbbb, j) <= at &&
-                    AT(S.sbody, j) != bi && !((gi != 0 && gi == gj) || ((gi | gj) & MG_GROUP_OFF)) &&
-                    !surely_apart(S, L, e, i, j)) {
-                    load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A);
+            int key = 0, ta = 0, bi = 0, tb = 0, bb = -1;
+            double ui = 0.0, ub = 0.0;
+            if (mine >= 0) {
+                int i = 0, k = w0 + mine;
+                while (k >= 4 + ns - 1 - i) { k -= 4 + ns - 1 - i; i++; }
+                bi = AT(S.sbody, i); ui = AT(S.su, i);
+                ta = AT(S.spoly, i) < 0 ? WS_CIRCLE : WS_POLY;
+                load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A);
+                if (k < 4) {
+                    load_wall(k, B);
+                    key = i * 128 + 100 + k; ub = 0.8; tb = WS_SEGMENT; bb = -1;
+                } else {
+                    const int j = i + 1 + (k - 4);
                     load_shape(S, L, e, j, (uint64_t)AT(S.shash, j), B);
-                    collide(A, B, info);
                     key = i * 128 + j; ub = AT(S.su, j); tb = B.type; bb = B.body;
                 }
+                collide(A, B, info);   // one call site: the narrowphase is inlined once
             }
-            // the chunk's contacts to lane 0, in candidate order
+            // the contacts to lane 0, in candidate order (= lane order: lane q holds the q-th hit)
             const uint32_t m = (uint32_t)(__ballot(info.count > 0) >> base) & ((1u << QL) - 1u);
             for (int s = 0; s < QL; s++) {
                 if (!((m >> s) & 1u)) continue;   // uniform over the env's lanes
@@ -93,14 +146,15 @@ MG_DEV void narrowphase_quad(const MGState &S, const mg_library *L, int e, int s
                 q.count = __shfl(info.count, src, 64);
                 q.n = v2(qshfl(info.n.x, src), qshfl(info.n.y, src));
 #pragma unroll
-                for (int k = 0; k < 2; k++) {
-                    q.p1[k] = v2(qshfl(info.p1[k].x, src), qshfl(info.p1[k].y, src));
-                    q.p2[k] = v2(qshfl(info.p2[k].x, src), qshfl(info.p2[k].y, src));
-                    q.hash[k] = qshfl_u64(info.hash[k], src);
+                for (int kk = 0; kk < 2; kk++) {
+                    q.p1[kk] = v2(qshfl(info.p1[kk].x, src), qshfl(info.p1[kk].y, src));
+                    q.p2[kk] = v2(qshfl(info.p2[kk].x, src), qshfl(info.p2[kk].y, src));
+                    q.hash[kk] = qshfl_u64(info.hash[kk], src);
                 }
-                const int qkey = __shfl(key, src, 64), qtb = __shfl(tb, src, 64), qbb = __shfl(bb, src, 64);
-                const double qub = qshfl(ub, src);
-                if (sub == 0) arbiter_update_t(S, L, e, qkey, ta, bi, qtb, qbb, ui, qub, q);
+                const int qkey = __shfl(key, src, 64), qta = __shfl(ta, src, 64), qbi = __shfl(bi, src, 64);
+                const int qtb = __shfl(tb, src, 64), qbb = __shfl(bb, src, 64);
+                const double qui = qshfl(ui, src), qub = qshfl(ub, src);
+                if (sub == 0) arbiter_update_t(S, L, e, qkey, qta, qbi, qtb, qbb, qui, qub, q);
             }
         }
     }
@@ -113,7 +167,8 @@ MG_DEV void space_step_quad(const MGState &S, const mg_library *L, int e, int su
     const uint32_t stamp = S.stamp[e] + 1;
     const int nact0 = S.nactive[e], nb = S.nbodies[e], ns = S.nshapes[e];
     for (int i = sub; i < nact0; i += QL) AT(S.astate, AT(S.active, i)) = ARB_NORMAL;
-    for (int b = sub; b < nb; b += QL) {
+    for (int p = sub; p < nb; p += QL) {
+        const int b = quad_body(p, nb);
         AT(S.bpx, b) = AT(S.bpx, b) + (AT(S.bvx, b) + AT(S.bvbx, b)) * dt;
         AT(S.bpy, b) = AT(S.bpy, b) + (AT(S.bvy, b) + AT(S.bvby, b)) * dt;
         body_set_angle_step(S, e, b, AT(S.ba, b) + (AT(S.bw, b) + AT(S.bwb, b)) * dt);
@@ -156,7 +211,7 @@ __device__ __forceinline__ void env_substeps_quad(const MGState &V, const mg_lib
     const double dt = L->dt;
     for (int i = 0; i < 10; i++) {
         __syncthreads();
-        if (sub == 0) robot_update(V, L, ev);
+        if (sub == 0) robot_update<true>(V, L, ev);
         MG_PP(P, 0);
         space_step_quad<NCS, QL, LDS_SHAPES>(V, L, ev, sub, dt, P);
     }

@@ -146,6 +146,34 @@ def frames_mode_bytes(preproc, world, n):
     return restack_ring_bytes(preproc, world, n) + 2 * len(stacked_keys(preproc)) * world * n * 4 * LOFR
 
 
+_HIP = None
+
+
+def _emulate_all_gather(recv, send, world, stream):
+    """bench.py --emulate-world: the receive-side HBM writes of an all-gather of `world` ranks, without peers --
+    `send` copied into each of the `world` blocks of `recv` by the DMA engines (hipMemcpyAsync
+    hipMemcpyDeviceToDeviceNoCU), as xGMI peer writes land in HBM without this GPU's compute units; falls back
+    to a copy kernel if the runtime refuses.  Returns which was used."""
+    global _HIP
+    import ctypes
+    nb = send.numel()
+    if _HIP is None:
+        try:
+            _HIP = ctypes.CDLL("libamdhip64.so")
+            _HIP.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                            ctypes.c_void_p]
+        except OSError:
+            _HIP = False
+    if _HIP:
+        rc = 0
+        for r in range(world):
+            rc = rc or _HIP.hipMemcpyAsync(recv.data_ptr() + r * nb, send.data_ptr(), nb, 1024, stream.cuda_stream)
+        if rc == 0:
+            return "sdma"
+    recv.view(world, -1).copy_(send.unsqueeze(0).expand(world, -1))
+    return "kernel"
+
+
 class NativeRestacker:
     """Receiver-side frame stacks of the frames-only gather on the GPU (mg_restack): keeps a ring of the
     last 4 frames of each stacked output's view for all W * n envs (restack_ring_bytes)."""
@@ -273,6 +301,7 @@ class ShardedVecEnv:
             self.t = 0
             self._ring_resets = None        # vec.reset_count at the last reset_async (frames mode: ring valid)
             self.restack_timing = False
+            self.emulated_copy = None
             self._restack_ev = []
 
     def enable_restack_timing(self):
@@ -314,7 +343,7 @@ class ShardedVecEnv:
                 if self.restacked[b] is not None:   # the restack of step t - 2 has read recv[b]
                     self.comm_stream.wait_event(self.restacked[b])
                 if self.emulate_world:
-                    recv.view(self.world, -1).copy_(send.unsqueeze(0).expand(self.world, -1))
+                    self.emulated_copy = _emulate_all_gather(recv, send, self.world, self.comm_stream)
                 else:
                     work = dist.all_gather_into_tensor(recv, send, async_op=True)
                     work.wait()   # the side stream (not the host) waits for the collective

@@ -124,9 +124,6 @@ KERNEL_FORMS = [
     # 4 lanes per env (16 envs per 64-lane workgroup; 70 envs leave shadow lanes in the last one)
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5"}),
     ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "6"}),
-    # the same with 8 / 4 envs per workgroup (8 / 16 lanes per env)
-    ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5", "MG_STEP_BLK": "8"}),
-    ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5", "MG_STEP_BLK": "4"}),
     ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "1"}),
     ("ClusterColour-Demo-LoResStack-v0", 66, 30, {"MG_STEP_VARIANT": "4"}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "4"}),
