@@ -1039,58 +1039,51 @@ MG_DEV void lground_apply(LaneBodies &R, const MGState &S, int e, int c, double 
 // the robot rows (3/4 of the sweep's time when read through readlane / lane-select) index bodies by
 // constants; block bodies stay in their lanes; arbiter rows reach a robot body through a uniform select.
 // Same operations in the same order as lcons_* / larb_*.
-MG_DEV double uget6(const double (&x)[6], int k) {
-    double r = x[0];
-#pragma unroll
-    for (int i = 1; i < 6; i++) r = k == i ? x[i] : r;
-    return r;
-}
-MG_DEV void uput6(double (&x)[6], int k, double v) {
-#pragma unroll
-    for (int i = 0; i < 6; i++) x[i] = k == i ? v : x[i];
-}
 MG_DEV bool is_rob(int b, int rb0) { return b >= rb0 && b < rb0 + 6; }
 // the robot's velocities, masses and joint accumulators (wave-uniform); the bias velocities (touched by
-// arbiter rows only) stay in the bodies' lanes
+// arbiter rows only) stay in the bodies' lanes.  Every access to RobotV uses a compile-time slot: a runtime
+// index (even through a select chain, which the compiler folds back into one) puts the whole struct in
+// per-lane scratch memory -- measured in round 3 as ~4 GB of scratch writes per launch at 8192 envs.
 struct RobotV { double vx[6], vy[6], w[6], minv[6], iinv[6], jacc[10], jacc2[10], twrn[10]; };
-MG_DEV double xget(double lf, const double (&rf)[6], int b, int rb0) {
-    if (b < 0) return 0.0;
-    if (is_rob(b, rb0)) return uget6(rf, b - rb0);
-    return rl_d(lf, b);
+// body side of an arbiter row: K >= 0 the robot's body slot K (in RobotV), K < 0 a block body (in its lane) or
+// the static body (b < 0)
+template <int K> MG_DEV double xget(double lf, const double (&rf)[6], int b) {
+    if constexpr (K >= 0) return rf[K];
+    else return b < 0 ? 0.0 : rl_d(lf, b);
 }
-MG_DEV void xput(double &lf, double (&rf)[6], int b, int rb0, int lane, double v) {
-    if (b < 0) return;
-    if (is_rob(b, rb0)) uput6(rf, b - rb0, v);
-    else lput(lf, b, lane, v);
+template <int K> MG_DEV void xput(double &lf, double (&rf)[6], int b, int lane, double v) {
+    if constexpr (K >= 0) rf[K] = v;
+    else if (b >= 0) lput(lf, b, lane, v);
 }
-MG_DEV void xapply(LaneBodies &R, RobotV &V, int rb0, int lane, int b, V2 j, V2 r) {
-    if (b < 0) return;
-    const double minv = xget(R.minv, V.minv, b, rb0), iinv = xget(R.iinv, V.iinv, b, rb0);
-    xput(R.vx, V.vx, b, rb0, lane, xget(R.vx, V.vx, b, rb0) + j.x * minv);
-    xput(R.vy, V.vy, b, rb0, lane, xget(R.vy, V.vy, b, rb0) + j.y * minv);
-    xput(R.w, V.w, b, rb0, lane, xget(R.w, V.w, b, rb0) + iinv * vcross(r, j));
+template <int K>
+MG_DEV void xapply(LaneBodies &R, RobotV &V, int lane, int b, V2 j, V2 r) {
+    if (K < 0 && b < 0) return;
+    const double minv = xget<K>(R.minv, V.minv, b), iinv = xget<K>(R.iinv, V.iinv, b);
+    xput<K>(R.vx, V.vx, b, lane, xget<K>(R.vx, V.vx, b) + j.x * minv);
+    xput<K>(R.vy, V.vy, b, lane, xget<K>(R.vy, V.vy, b) + j.y * minv);
+    xput<K>(R.w, V.w, b, lane, xget<K>(R.w, V.w, b) + iinv * vcross(r, j));
 }
-MG_DEV void xapply_bias(LaneBodies &R, RobotV &V, int rb0, int lane, int b, V2 j, V2 r) {
+template <int K>
+MG_DEV void xapply_bias(LaneBodies &R, RobotV &V, int lane, int b, V2 j, V2 r) {
     if (b < 0) return;
-    const double minv = xget(R.minv, V.minv, b, rb0), iinv = xget(R.iinv, V.iinv, b, rb0);
+    const double minv = xget<K>(R.minv, V.minv, b), iinv = xget<K>(R.iinv, V.iinv, b);
     lput(R.vbx, b, lane, lget(R.vbx, b) + j.x * minv);
     lput(R.vby, b, lane, lget(R.vby, b) + j.y * minv);
     lput(R.wb, b, lane, lget(R.wb, b) + iinv * vcross(r, j));
 }
-MG_DEV void xarb_cached(LaneBodies &R, RobotV &V, int rb0, int lane, const MGState &S, int e, int slot,
-                        double dt_coef) {
-    if (ufirst(AT(S.astate, slot)) == ARB_FIRST) return;
-    const int a = ufirst(AT(S.asa, slot)), b = ufirst(AT(S.asb, slot));
+template <int KA, int KB>
+MG_DEV void xarb_cached_k(LaneBodies &R, RobotV &V, int lane, const MGState &S, int e, int slot, int a, int b,
+                          double dt_coef) {
     V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
     const int cnt = ufirst(AT(S.acount, slot));
     for (int k = 0; k < cnt; k++) {
         V2 j = vmult(vrotate(n, v2(ACON(k, AC_JN, slot), ACON(k, AC_JT, slot))), dt_coef);
-        xapply(R, V, rb0, lane, a, vneg(j), v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)));
-        xapply(R, V, rb0, lane, b, j, v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot)));
+        xapply<KA>(R, V, lane, a, vneg(j), v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)));
+        xapply<KB>(R, V, lane, b, j, v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot)));
     }
 }
-MG_DEV void xarb_apply(LaneBodies &R, RobotV &V, int rb0, int lane, const MGState &S, int e, int slot) {
-    const int a = ufirst(AT(S.asa, slot)), b = ufirst(AT(S.asb, slot));
+template <int KA, int KB>
+MG_DEV void xarb_apply_k(LaneBodies &R, RobotV &V, int lane, const MGState &S, int e, int slot, int a, int b) {
     V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
     double friction = AT(S.au, slot);
     const int cnt = ufirst(AT(S.acount, slot));
@@ -1099,8 +1092,8 @@ MG_DEV void xarb_apply(LaneBodies &R, RobotV &V, int rb0, int lane, const MGStat
         V2 r1 = v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)), r2 = v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot));
         V2 vb1 = vadd(v2(lget(R.vbx, a), lget(R.vby, a)), vmult(vperp(r1), lget(R.wb, a)));
         V2 vb2 = vadd(v2(lget(R.vbx, b), lget(R.vby, b)), vmult(vperp(r2), lget(R.wb, b)));
-        V2 v1 = vadd(v2(xget(R.vx, V.vx, a, rb0), xget(R.vy, V.vy, a, rb0)), vmult(vperp(r1), xget(R.w, V.w, a, rb0)));
-        V2 v2_ = vadd(v2(xget(R.vx, V.vx, b, rb0), xget(R.vy, V.vy, b, rb0)), vmult(vperp(r2), xget(R.w, V.w, b, rb0)));
+        V2 v1 = vadd(v2(xget<KA>(R.vx, V.vx, a), xget<KA>(R.vy, V.vy, a)), vmult(vperp(r1), xget<KA>(R.w, V.w, a)));
+        V2 v2_ = vadd(v2(xget<KB>(R.vx, V.vx, b), xget<KB>(R.vy, V.vy, b)), vmult(vperp(r2), xget<KB>(R.w, V.w, b)));
         V2 vr = vsub(v2_, v1);
         double vbn = vdot(vsub(vb2, vb1), n);
         double vrn = vdot(vr, n);
@@ -1117,12 +1110,34 @@ MG_DEV void xarb_apply(LaneBodies &R, RobotV &V, int rb0, int lane, const MGStat
         double jtAcc = cpclamp(jtOld + jt, -jtMax, jtMax);
         if (lane == 0) { ACON(k, AC_JB, slot) = jBias; ACON(k, AC_JN, slot) = jnAcc; ACON(k, AC_JT, slot) = jtAcc; }
         V2 jb = vmult(n, jBias - jbnOld);
-        xapply_bias(R, V, rb0, lane, a, vneg(jb), r1);
-        xapply_bias(R, V, rb0, lane, b, jb, r2);
+        xapply_bias<KA>(R, V, lane, a, vneg(jb), r1);
+        xapply_bias<KB>(R, V, lane, b, jb, r2);
         V2 j = vrotate(n, v2(jnAcc - jnOld, jtAcc - jtOld));
-        xapply(R, V, rb0, lane, a, vneg(j), r1);
-        xapply(R, V, rb0, lane, b, j, r2);
+        xapply<KA>(R, V, lane, a, vneg(j), r1);
+        xapply<KB>(R, V, lane, b, j, r2);
     }
+}
+// Arbiter rows dispatched on their bodies' robot slots (uniform branches, so every RobotV access has a constant
+// slot): only the bodies that carry shapes can be in contact -- the robot body (slot 0) and the fingers (4, 5)
+// -- and robot shapes never collide with each other (one shape group), so (a, b) is one of block / robot
+// body / finger with a block or the static body.  Any other pair would be a scene outside the compiled robot
+// rows: flagged (error 32), never expected.
+template <bool CACHED>
+MG_DEV void xarb_row(LaneBodies &R, RobotV &V, int rb0, int lane, const MGState &S, int e, int slot, double x) {
+    if (CACHED && ufirst(AT(S.astate, slot)) == ARB_FIRST) return;
+    const int a = ufirst(AT(S.asa, slot)), b = ufirst(AT(S.asb, slot));
+    const int ka = is_rob(a, rb0) ? a - rb0 : -1, kb = is_rob(b, rb0) ? b - rb0 : -1;
+#define XROW(KA, KB) do { if (CACHED) xarb_cached_k<KA, KB>(R, V, lane, S, e, slot, a, b, x); \
+                          else xarb_apply_k<KA, KB>(R, V, lane, S, e, slot, a, b); } while (0)
+    if (ka < 0 && kb < 0) XROW(-1, -1);
+    else if (kb < 0 && ka == 0) XROW(0, -1);
+    else if (kb < 0 && ka == 4) XROW(4, -1);
+    else if (kb < 0 && ka == 5) XROW(5, -1);
+    else if (ka < 0 && kb == 0) XROW(-1, 0);
+    else if (ka < 0 && kb == 4) XROW(-1, 4);
+    else if (ka < 0 && kb == 5) XROW(-1, 5);
+    else if (lane == 0) S.overflow[e] |= 32;
+#undef XROW
 }
 // robot joint K (static_cons(K): compile-time type and body slots) at list index c: lcons_cached /
 // lcons_apply with the bodies and accumulators in registers and the pre-stepped terms read from LDS
@@ -1400,7 +1415,7 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
             V.jacc2[k] = static_cons(k).type == MG_C_PIVOT ? CPA(CP_JACC2, rc0 + k) : 0.0;
             V.twrn[k] = static_cons(k).type == MG_C_SPRING ? CPA(CP_TWRN, rc0 + k) : 0.0;
         }
-        for (int i = 0; i < unact; i++) xarb_cached(R, V, rb0, lane, S, e, ufirst(AT(S.active, i)), dt_coef);
+        for (int i = 0; i < unact; i++) xarb_row<true>(R, V, rb0, lane, S, e, ufirst(AT(S.active, i)), dt_coef);
         if (G.n > 0) {
             lground_cached(R, S, e, G.c0, dt_coef);
             if (G.n > 1) lground_cached(R, S, e, G.c1, dt_coef);
@@ -1410,7 +1425,7 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
 #pragma unroll 1
         for (int it = 0; it < MG_EXP_COOP_ITERS; it++) {
 #ifndef MG_EXP_COOP_NOARB
-            for (int i = 0; i < unact; i++) xarb_apply(R, V, rb0, lane, S, e, ufirst(AT(S.active, i)));
+            for (int i = 0; i < unact; i++) xarb_row<false>(R, V, rb0, lane, S, e, ufirst(AT(S.active, i)), 0.0);
 #endif
 #ifndef MG_EXP_COOP_NOGROUND
             if (G.n > 0) {
@@ -1424,10 +1439,11 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
         }
         // robot lanes: velocities from V (their bias velocities stayed in the lanes)
         if (lane < nb) {
-            const bool rob = is_rob(lane, rb0);
-            const int k = rob ? lane - rb0 : 0;
-            AT(S.bvx, lane) = rob ? uget6(V.vx, k) : R.vx; AT(S.bvy, lane) = rob ? uget6(V.vy, k) : R.vy;
-            AT(S.bw, lane) = rob ? uget6(V.w, k) : R.w;
+            double vx = R.vx, vy = R.vy, w = R.w;
+#pragma unroll
+            for (int k = 0; k < 6; k++)   // constant slots (see RobotV)
+                if (lane == rb0 + k) { vx = V.vx[k]; vy = V.vy[k]; w = V.w[k]; }
+            AT(S.bvx, lane) = vx; AT(S.bvy, lane) = vy; AT(S.bw, lane) = w;
             AT(S.bvbx, lane) = R.vbx; AT(S.bvby, lane) = R.vby; AT(S.bwb, lane) = R.wb;
         }
         if (lane == 0) {
