@@ -23,12 +23,12 @@ the whole node's step results -- is one all-gather per step:
   restarts its stacks: its frame is the next episode's first).  The simulator
   binds its outputs in frames-only mode, so it writes no stacks of its own.
   gather_mode "stacked" gathers the preprocessor's whole outputs instead;
-* two buffer sets alternate between steps; the collective runs on its own HIP
-  stream and the restack on a third (in step order), so the exchange of step t
-  overlaps the compute of step t + 1 and the restack of step t (HBM-bound)
-  overlaps the all-gather of step t + 1 (xGMI-bound)
-  (ShardedVecEnv.step_async).  A step's gathered views stay valid until the
-  step after next.
+* `nbuf` buffer sets (default 3) rotate between steps; the collective runs on its
+  own HIP stream and the restack on a third (in step order), so the exchange of
+  step t overlaps the compute of steps t + 1 .. t + nbuf - 1 and the restack of
+  step t (HBM-bound) overlaps the all-gather of step t + 1 (xGMI-bound)
+  (ShardedVecEnv.step_async).  A step's gathered views stay valid for the next
+  nbuf - 1 steps.
 """
 import collections
 
@@ -140,10 +140,10 @@ def restack_ring_bytes(preproc, world, n):
     return len(stacked_keys(preproc)) * 4 * world * n * LOFR
 
 
-def frames_mode_bytes(preproc, world, n):
-    """Receiver-side device memory of gather_mode 'frames' per rank: the ring plus two sets of rebuilt
-    stacks (u8[W * n][96][96][12] per stacked key, one set per alternating buffer set)."""
-    return restack_ring_bytes(preproc, world, n) + 2 * len(stacked_keys(preproc)) * world * n * 4 * LOFR
+def frames_mode_bytes(preproc, world, n, nbuf=3):
+    """Receiver-side device memory of gather_mode 'frames' per rank: the ring plus nbuf sets of rebuilt
+    stacks (u8[W * n][96][96][12] per stacked key, one set per rotating buffer set)."""
+    return restack_ring_bytes(preproc, world, n) + nbuf * len(stacked_keys(preproc)) * world * n * 4 * LOFR
 
 
 _HIP = None
@@ -249,7 +249,7 @@ class ShardedVecEnv:
     reset directly (vec.reset()), since the other ranks' rings would then hold stale frames of its envs."""
 
     def __init__(self, env_name, envs_per_rank, rank=None, device=None, base_seed=1000, gather=False, vec=None,
-                 gather_mode=None, restacker=None, max_episode_steps=None, emulate_world=None):
+                 gather_mode=None, restacker=None, max_episode_steps=None, emulate_world=None, nbuf=3):
         from . import registry
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if dist.is_initialized() else 1
@@ -281,23 +281,28 @@ class ShardedVecEnv:
             self.layout = PackedLayout.for_spec(spec, envs_per_rank, frames_only=frames)
             self.stacked_nbytes = PackedLayout.for_spec(spec, envs_per_rank).nbytes
             self.device = dev
-            self.send = [torch.empty(self.layout.nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
-            self.recv = [torch.empty(self.world * self.layout.nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
-            self.stacks = [None, None]
+            # nbuf buffer sets: the compute of step t + nbuf - 1 may start before the exchange of step t is done
+            # (measured with 8 emulated ranks, round 4: the exchange of a step takes longer than its compute)
+            self.nbuf = nb = int(nbuf)
+            if nb < 2:
+                raise ValueError("nbuf must be >= 2")
+            self.send = [torch.empty(self.layout.nbytes, dtype=torch.uint8, device=dev) for _ in range(nb)]
+            self.recv = [torch.empty(self.world * self.layout.nbytes, dtype=torch.uint8, device=dev) for _ in range(nb)]
+            self.stacks = [None] * nb
             if frames:
                 wn = self.world * envs_per_rank
                 self.stacks = [collections.OrderedDict((k, torch.empty((wn, 96, 96, 12), dtype=torch.uint8, device=dev))
-                                                       for k in stacked_keys(spec.preproc)) for _ in range(2)]
+                                                       for k in stacked_keys(spec.preproc)) for _ in range(nb)]
                 if restacker is None:
                     if dev.type != "cuda":
                         raise ValueError("gather_mode 'frames' on CPU tensors needs a restacker")
                     restacker = NativeRestacker(self.layout, self.world, dev)
             self.restacker = restacker
-            self.pending = [None, None]
+            self.pending = [None] * nb
             self.comm_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
             # the restack has its own stream: restack(t) (HBM-bound) overlaps gather(t + 1) (xGMI-bound)
             self.restack_stream = torch.cuda.Stream(dev) if dev.type == "cuda" and frames else None
-            self.restacked = [None, None]   # per buffer set: event after the restack that last read recv[b]
+            self.restacked = [None] * nb    # per buffer set: event after the restack that last read recv[b]
             self.t = 0
             self._ring_resets = None        # vec.reset_count at the last reset_async (frames mode: ring valid)
             self.restack_timing = False
@@ -320,7 +325,7 @@ class ShardedVecEnv:
     # -- packed gather pipeline ---------------------------------------------------------------------------
     def _begin(self):
         """Buffer set of this step: the exchange that last used it (two steps ago) must be done first."""
-        b = self.t % 2
+        b = self.t % self.nbuf
         if self.pending[b] is not None:
             self.pending[b].wait()
             self.pending[b] = None
