@@ -19,6 +19,14 @@
 #pragma once
 #include "mg_step.h"
 
+// Lane layout of the 64-lane wavefront: env ev (0 .. 64/QL - 1) and its sub-lane s (0 .. QL - 1).  Default:
+// interleaved, lane = ev * QL + s.  MG_QUAD_PACKED: lane = ev + s * (64 / QL), so the sub-lane-0 lanes that
+// run the serial parts (solver, arbiter updates, springs) are the wave's first 64 / QL lanes.
+#ifndef MG_QUAD_PACKED
+#define MG_QUAD_PACKED 0
+#endif
+template <int QL> MG_DEV int qlane(int ev, int s) { return MG_QUAD_PACKED ? ev + s * (64 / QL) : ev * QL + s; }
+
 // 64-bit values across lanes (ds_bpermute on the two halves)
 MG_DEV double qshfl(double v, int src) {
     const uint64_t u = __double_as_longlong(v);
@@ -89,7 +97,6 @@ MG_DEV void narrowphase_quad(const MGState &S, const mg_library *L, int e, int s
     ShapeW locA, locB;
     ShapeW &A = LDS_SHAPES ? S.shw[2 * QL * e + 2 * sub] : locA;
     ShapeW &B = LDS_SHAPES ? S.shw[2 * QL * e + 2 * sub + 1] : locB;
-    const int base = (int)(threadIdx.x & 63) - sub;   // the env's lane 0
     const int ntot = 4 * ns + (ns * (ns - 1)) / 2;
     for (int w0 = 0; w0 < ntot; w0 += 64) {
         const int wn = ntot - w0 < 64 ? ntot - w0 : 64;
@@ -104,7 +111,8 @@ MG_DEV void narrowphase_quad(const MGState &S, const mg_library *L, int e, int s
             }
         }
 #pragma unroll
-        for (int off = 1; off < QL; off <<= 1) hits |= qshfl_xor_u64(hits, off);   // the env's lanes: disjoint bits
+        for (int off = 1; off < QL; off <<= 1)   // the env's lanes: disjoint bits
+            hits |= qshfl_xor_u64(hits, MG_QUAD_PACKED ? off * (64 / QL) : off);
         // pass 2
         while (hits) {   // uniform over the env's lanes
             uint64_t rest = hits;
@@ -138,10 +146,13 @@ MG_DEV void narrowphase_quad(const MGState &S, const mg_library *L, int e, int s
                 collide(A, B, info);   // one call site: the narrowphase is inlined once
             }
             // the contacts to lane 0, in candidate order (= lane order: lane q holds the q-th hit)
-            const uint32_t m = (uint32_t)(__ballot(info.count > 0) >> base) & ((1u << QL) - 1u);
+            const uint64_t bal = __ballot(info.count > 0);
+            uint32_t m = 0;
+#pragma unroll
+            for (int s = 0; s < QL; s++) m |= (uint32_t)((bal >> qlane<QL>(e, s)) & 1ull) << s;
             for (int s = 0; s < QL; s++) {
                 if (!((m >> s) & 1u)) continue;   // uniform over the env's lanes
-                const int src = base + s;
+                const int src = qlane<QL>(e, s);
                 Collision q;
                 q.count = __shfl(info.count, src, 64);
                 q.n = v2(qshfl(info.n.x, src), qshfl(info.n.y, src));

@@ -16,10 +16,19 @@ line() { python3 -c "import json; d=json.loads(open('$OUT/$1.log').read().strip(
 if [ "$SKIP" != 1 ]; then
   run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 fi
+if [ -x tools/ubench/exec_f64 ]; then
+  timeout -k 10 60 ./tools/ubench/exec_f64 256 > "$OUT/ubench_exec.log" 2>&1 && cat "$OUT/ubench_exec.log"
+fi
+if [ -f magical-1_amd/magical_amd/libmagical_sim_packed.so ]; then   # A/B: packed quad lane layout
+  MAGICAL_AMD_EXP_LIB=packed run pytest_packed 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "step_kernel_forms and (MoveTo)" --timeout 120 --timeout-method thread
+  for env in MoveToRegion-Demo-LoRes4E-v0 MoveToCorner-Demo-LoRes4E-v0; do
+    MAGICAL_AMD_EXP_LIB=packed run packed.$env 300 python bench.py --env $env --envs 4096 --steps 60 --warmup 10 --no-cpu-baseline && line packed.$env
+  done
+fi
 for cfg in MoveToRegion-Demo-LoRes4E-v0:4096 MoveToCorner-Demo-LoRes4E-v0:4096 ClusterColour-Demo-LoResStack-v0:8192 MatchRegions-TestAll-LoRes4E-v0:8192; do
   env=${cfg%%:*}; n=${cfg##*:}
   run bench.$env 300 python bench.py --env $env --envs $n --steps 60 --warmup 10 --no-cpu-baseline && line bench.$env
 done
-for cap in 0 256 1024; do
+for cap in 0; do
   MG_RESTACK_WGS=$cap run emul8.cap$cap 300 python bench.py --envs 4096 --steps 40 --warmup 10 --no-cpu-baseline --emulate-world 8 && line emul8.cap$cap
 done
