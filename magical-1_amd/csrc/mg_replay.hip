@@ -129,9 +129,10 @@ __global__ __launch_bounds__(256) void replay_assemble_kernel(const uint8_t *__r
 // frame, as the deques of benchmarks/__init__.py:75-82,139-147 are filled at reset.  Byte work per env and
 // stack: 1 frame read (+ 3 ring frames unless fresh), 1 ring frame written and the 4-frame stack written --
 // HBM bound (the stack and ring with non-temporal stores: nothing re-reads them this step).
-__device__ __forceinline__ void nt_store16(uint4 *p, uint4 v) {
-    __builtin_nontemporal_store(v.x, &((uint32_t *)p)[0]); __builtin_nontemporal_store(v.y, &((uint32_t *)p)[1]);
-    __builtin_nontemporal_store(v.z, &((uint32_t *)p)[2]); __builtin_nontemporal_store(v.w, &((uint32_t *)p)[3]);
+typedef unsigned int mg_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void nt_store16(uint4 *p, uint4 v) {   // one 16-byte non-temporal store
+    mg_u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (mg_u32x4 *)p);
 }
 __device__ __forceinline__ void load48(const uint8_t *src, uint32_t (&w)[12]) {
     const uint4 *s4 = (const uint4 *)src;
