@@ -180,9 +180,8 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
     constexpr bool QUAD = VAR == 5 || VAR == 6; // QL lanes per env, BLK envs in one 64-lane workgroup
     constexpr int QL = QUAD ? 64 / BLK : 1;
     constexpr int NCS = VAR == 3 || VAR == 4 ? 0 : C.nc; // compile-time constraint list (0: the env's runtime list)
-    const int lane = COOP ? (int)threadIdx.x : QUAD ? (MG_QUAD_PACKED ? (int)threadIdx.x % BLK : (int)threadIdx.x / QL)
-                   : BLK == 1 ? 0 : (int)threadIdx.x;
-    const int sub = QUAD ? (MG_QUAD_PACKED ? (int)threadIdx.x / BLK : (int)threadIdx.x % QL) : 0;
+    const int lane = COOP ? (int)threadIdx.x : QUAD ? (int)threadIdx.x / QL : BLK == 1 ? 0 : (int)threadIdx.x;
+    const int sub = QUAD ? (int)threadIdx.x % QL : 0;
     int e = xcd_block(blockIdx.x, gridDim.x) * BLK + (COOP ? 0 : lane);
     // QUAD: lanes without an env of their own (past n_envs, or a scene the form cannot hold) still take
     // part in the workgroup barriers as shadows of a valid env; they never write HBM

@@ -19,13 +19,10 @@
 #pragma once
 #include "mg_step.h"
 
-// Lane layout of the 64-lane wavefront: env ev (0 .. 64/QL - 1) and its sub-lane s (0 .. QL - 1).  Default:
-// interleaved, lane = ev * QL + s.  MG_QUAD_PACKED: lane = ev + s * (64 / QL), so the sub-lane-0 lanes that
-// run the serial parts (solver, arbiter updates, springs) are the wave's first 64 / QL lanes.
-#ifndef MG_QUAD_PACKED
-#define MG_QUAD_PACKED 0
-#endif
-template <int QL> MG_DEV int qlane(int ev, int s) { return MG_QUAD_PACKED ? ev + s * (64 / QL) : ev * QL + s; }
+// Lane layout: env ev (0 .. 64/QL - 1) of the wavefront owns lanes ev * QL .. ev * QL + QL - 1 (a layout with
+// the serial sub-lane-0 lanes packed first in the wave measured the same, round 4: FP64 instructions cost the
+// same whatever the number of active lanes -- tools/ubench/exec_f64.hip)
+template <int QL> MG_DEV int qlane(int ev, int s) { return ev * QL + s; }
 
 // 64-bit values across lanes (ds_bpermute on the two halves)
 MG_DEV double qshfl(double v, int src) {
@@ -112,7 +109,7 @@ MG_DEV void narrowphase_quad(const MGState &S, const mg_library *L, int e, int s
         }
 #pragma unroll
         for (int off = 1; off < QL; off <<= 1)   // the env's lanes: disjoint bits
-            hits |= qshfl_xor_u64(hits, MG_QUAD_PACKED ? off * (64 / QL) : off);
+            hits |= qshfl_xor_u64(hits, off);
         // pass 2
         while (hits) {   // uniform over the env's lanes
             uint64_t rest = hits;
