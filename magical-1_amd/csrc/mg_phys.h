@@ -40,8 +40,8 @@ MG_DEV double cpclamp(double f, double mn, double mx) { return cpmin(cpmax(f, mn
 MG_DEV double cpclamp01(double f) { return cpmax(0.0, cpmin(f, 1.0)); }
 MG_DEV uint64_t hash_pair(uint64_t a, uint64_t b) { return (a * 3344921057ull) ^ (b * 3344921057ull); }
 
-// arena walls (entities.py:510-522): static segments, radius 1, friction 0.8
-__constant__ static const double MG_WALL[4][4] = {{-2, 2, 2, 2}, {2, 2, 2, -2}, {2, -2, -2, -2}, {-2, -2, -2, 2}};
+// arena walls (entities.py:510-522): static segments, radius 1, friction 0.8, end points
+// {(-2,2)-(2,2), (2,2)-(2,-2), (2,-2)-(-2,-2), (-2,-2)-(-2,2)} (wall_a / wall_b below)
 
 // --------------------------------------------------------------------------
 // body helpers
@@ -82,10 +82,13 @@ struct ShapeW {
     double bbl, bbb, bbr, bbt;
 };
 
+// wall w's end points (as arithmetic on w: no constant-memory load on the narrowphase's path)
+MG_DEV V2 wall_a(int w) { return v2(w == 0 || w == 3 ? -2.0 : 2.0, w >= 2 ? -2.0 : 2.0); }
+MG_DEV V2 wall_b(int w) { return v2(w <= 1 ? 2.0 : -2.0, w == 1 || w == 2 ? -2.0 : 2.0); }
 MG_DEV void load_wall(int w, ShapeW &sh) {
     sh.type = WS_SEGMENT; sh.count = 0; sh.body = -1; sh.hashid = (uint64_t)w; sh.r = 1.0;
     // identity transform of the (never positioned) static arena body: {1, 0, -0, 1, 0, 0}
-    V2 a = v2(MG_WALL[w][0], MG_WALL[w][1]), b = v2(MG_WALL[w][2], MG_WALL[w][3]);
+    V2 a = wall_a(w), b = wall_b(w);
     sh.a = v2(1.0 * a.x + (-0.0) * a.y + 0.0, 0.0 * a.x + 1.0 * a.y + 0.0);
     sh.b = v2(1.0 * b.x + (-0.0) * b.y + 0.0, 0.0 * b.x + 1.0 * b.y + 0.0);
     V2 n = vrperp(vnormalize(vsub(b, a)));
@@ -163,7 +166,8 @@ MG_DEV void shape_update_bb(const MGState &S, const mg_library *L, int e, int k)
 
 // BB of arena wall w (load_wall: segment a-b of radius 1)
 MG_DEV void wall_bb(int w, double &l, double &b, double &r, double &t) {
-    const double ax = MG_WALL[w][0], ay = MG_WALL[w][1], bx = MG_WALL[w][2], by = MG_WALL[w][3];
+    const V2 wa = wall_a(w), wb = wall_b(w);
+    const double ax = wa.x, ay = wa.y, bx = wb.x, by = wb.y;
     l = (ax < bx ? ax : bx) - 1.0; r = (ax < bx ? bx : ax) + 1.0;
     b = (ay < by ? ay : by) - 1.0; t = (ay < by ? by : ay) + 1.0;
 }

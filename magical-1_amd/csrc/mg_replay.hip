@@ -123,28 +123,19 @@ __global__ __launch_bounds__(256) void replay_assemble_kernel(const uint8_t *__r
 }
 
 // Receiver-side frame stacks of the compact multi-GPU gather (mg_restack, magical_amd.dist): one thread per
-// 16 pixels of one env and one output stack (blockIdx.y: LoResStack 0 allo / 1 ego; else 0 = past_obs), all
-// accesses 16 B wide (16 px x 3 B = 3 x 16 B per frame).  The ring view of the stack keeps the env's last 4
-// frames (slot t % 4 = this step); a fresh env (reset, or done = auto-reset) fills every slot with its current
-// frame, as the deques of benchmarks/__init__.py:75-82,139-147 are filled at reset.  Byte work per env and
-// stack: 1 frame read (+ 3 ring frames unless fresh), 1 ring frame written and the 4-frame stack written --
-// HBM bound (the stack and ring with non-temporal stores: nothing re-reads them this step).
-typedef unsigned int mg_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void nt_store16(uint4 *p, uint4 v) {   // one 16-byte non-temporal store
-    mg_u32x4 w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, (mg_u32x4 *)p);
-}
-__device__ __forceinline__ void load48(const uint8_t *src, uint32_t (&w)[12]) {
-    const uint4 *s4 = (const uint4 *)src;
-#pragma unroll
-    for (int k = 0; k < 3; k++) { const uint4 v = s4[k]; w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w; }
-}
+// 4 pixels of one env and one output stack (blockIdx.y: LoResStack 0 allo / 1 ego; else 0 = past_obs).
+// The ring view of the stack keeps the env's last 4 frames (slot t % 4 = this step); a fresh env (reset,
+// or done = auto-reset) fills every slot with its current frame, as the deques of
+// benchmarks/__init__.py:75-82,139-147 are filled at reset.  Byte work: per env and stack 12 B read (+ 36 B
+// of ring unless fresh), 12 B ring write and 48 B stacked output per 4 pixels -- HBM bound.  (A 16-pixel
+// form with 16-byte accesses measured 5x slower, round 4: each store instruction then writes 16 B into 64
+// different cache lines, 192 B apart; here 3 back-to-back stores complete the lines.)
 __global__ __launch_bounds__(256) void restack_kernel(const uint8_t *__restrict__ recv, uint32_t world, uint32_t n,
                                                       int64_t stride, int64_t off_a, int64_t off_e, int64_t off_d,
                                                       int32_t preproc, uint32_t slot, int32_t all_fresh,
                                                       uint8_t *__restrict__ ring, uint8_t *__restrict__ out0,
                                                       uint8_t *__restrict__ out1) {
-    constexpr uint32_t Q = LO * LO / 16;   // 16-pixel units per frame
+    constexpr uint32_t Q = LO * LO / 4;
     const uint32_t W = world * n;
     const int s = blockIdx.y;
     // grid-stride (a capped grid leaves the SIMDs' register files to the simulator's kernels, MG_RESTACK_WGS)
@@ -155,42 +146,39 @@ __global__ __launch_bounds__(256) void restack_kernel(const uint8_t *__restrict_
         const bool fresh = all_fresh || blk[off_d + i] != 0;
         // the view this stack's frames come from (LoRes3EA: ego, with the current allo frame in slot 0)
         const int rv = (preproc == MG_PREPROC_LORES4A || (preproc == MG_PREPROC_LORESSTACK && s == 0)) ? 0 : 1;
-        const size_t po = (size_t)q * 48;
+        const size_t po = (size_t)q * 12;
+        const uint32_t *cur = (const uint32_t *)(blk + (rv ? off_e : off_a) + (size_t)i * LOFR + po);
         uint8_t *rring = ring + (size_t)s * 4 * W * LOFR;   // one ring per output stack (LoResStack: 2, else 1)
-        auto rslot = [&](uint32_t sl) { return rring + ((size_t)(sl & 3) * W + g) * LOFR + po; };
-        uint32_t f[4][12];
-        load48(blk + (rv ? off_e : off_a) + (size_t)i * LOFR + po, f[3]);
+        auto rslot = [&](uint32_t sl) { return (uint32_t *)(rring + ((size_t)(sl & 3) * W + g) * LOFR + po); };
+        uint32_t f[4][3];
+#pragma unroll
+        for (int w = 0; w < 3; w++) f[3][w] = cur[w];
         if (fresh) {
 #pragma unroll
             for (int k = 0; k < 3; k++)
 #pragma unroll
-                for (int w = 0; w < 12; w++) f[k][w] = f[3][w];
+                for (int w = 0; w < 3; w++) f[k][w] = f[3][w];
+#pragma unroll
+            for (uint32_t sl = 0; sl < 4; sl++) {
+                uint32_t *d = rslot(sl);
+                d[0] = f[3][0]; d[1] = f[3][1]; d[2] = f[3][2];
+            }
         } else {
 #pragma unroll
-            for (int k = 0; k < 3; k++) load48(rslot(slot + 1 + k), f[k]);   // stack slot k = frame t - (3 - k)
+            for (int k = 0; k < 3; k++) {          // stack slot k = frame t - (3 - k)
+                const uint32_t *src = rslot(slot + 1 + k);
+#pragma unroll
+                for (int w = 0; w < 3; w++) f[k][w] = src[w];
+            }
+            uint32_t *d = rslot(slot);
+            d[0] = f[3][0]; d[1] = f[3][1]; d[2] = f[3][2];
         }
+        if (preproc == MG_PREPROC_LORES3EA) {      // allo depth 1 in front of the ego frames t-2, t-1, t
+            const uint32_t *a = (const uint32_t *)(blk + off_a + (size_t)i * LOFR + po);
 #pragma unroll
-        for (uint32_t sl = 0; sl < 4; sl++) {
-            if (!fresh && sl != (slot & 3)) continue;
-            uint4 *d = (uint4 *)rslot(sl);
-#pragma unroll
-            for (int k = 0; k < 3; k++) nt_store16(d + k, make_uint4(f[3][4 * k], f[3][4 * k + 1], f[3][4 * k + 2], f[3][4 * k + 3]));
+            for (int w = 0; w < 3; w++) f[0][w] = a[w];
         }
-        if (preproc == MG_PREPROC_LORES3EA)   // allo depth 1 in front of the ego frames t-2, t-1, t
-            load48(blk + off_a + (size_t)i * LOFR + po, f[0]);
-        uint8_t *dst = (s ? out1 : out0) + (size_t)g * LOFR * 4 + po * 4;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {   // 4 pixels at a time: 3 dwords of each frame -> 48 B of stack
-            uint32_t f4[4][3];
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-#pragma unroll
-                for (int w = 0; w < 3; w++) f4[k][w] = f[k][3 * u + w];
-            uint4 o[3];
-            stack_pack(f4, o);
-#pragma unroll
-            for (int k = 0; k < 3; k++) nt_store16((uint4 *)(dst + 48 * u) + k, o[k]);
-        }
+        stack_regs(f, (s ? out1 : out0) + (size_t)g * LOFR * 4 + po * 4);
     }
 }
 }  // namespace
@@ -215,7 +203,7 @@ extern "C" hipError_t mg_launch_restack(const uint8_t *recv, int32_t world, int3
                                         int64_t off_e, int64_t off_d, int32_t preproc, int64_t step, int32_t all_fresh,
                                         uint8_t *ring, uint8_t *out_allo, uint8_t *out_ego, uint8_t *out_past,
                                         hipStream_t st) {
-    const int64_t t = (int64_t)world * n * (LO * LO / 16);
+    const int64_t t = (int64_t)world * n * (LO * LO / 4);
     const bool two = preproc == MG_PREPROC_LORESSTACK;
     int64_t wgs = (t + 255) / 256;
     static const int64_t cap = getenv("MG_RESTACK_WGS") ? atoll(getenv("MG_RESTACK_WGS")) : 0;   // experiments
