@@ -235,6 +235,10 @@ def main():
                     help="one GPU runs rank 0 of a W-rank node's exchange: each step's frames-only buffer is copied "
                          "into all W receive blocks (standing in for the all-gather) and restacked for W x envs on "
                          "the restack stream, beside the next step (value stays this rank's env-steps/s x W)")
+    ap.add_argument("--chunks", default="auto",
+                    help="env chunks pipelined on their own HIP streams (magical_amd.pipeline): an int, or auto = "
+                         "2 for the robot scenes (MoveToRegion / MoveToCorner: measured faster), 1 otherwise and "
+                         "under the all-gather")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -276,7 +280,7 @@ def main():
     import torch
     import torch.distributed as dist
     import magical_amd
-    from magical_amd import native, registry
+    from magical_amd import native, pipeline, registry
 
     spec = registry.lookup(args.env)
     device = torch.device("cuda", local_rank)
@@ -293,7 +297,13 @@ def main():
                                     gather_mode=args.gather_mode, emulate_world=emulate or None)
         vec = shard.vec
         step = shard.step_async
-    else:
+    chunks = 1
+    if not gather:
+        chunks = int(args.chunks) if args.chunks != "auto" else pipeline.default_chunks(spec, n)
+    if chunks > 1:
+        vec = pipeline.PipelinedVecEnv(args.env, n, chunks=chunks, device=str(device), seeds=seeds)
+        step = vec.step
+    elif not gather:
         vec = magical_amd.make_vec(args.env, n, device=str(device), seeds=seeds)
         step = vec.step
     lib = vec.lib
@@ -311,8 +321,13 @@ def main():
         step(actions)
     if gather:
         shard.wait_all()
+    if chunks > 1:
+        vec.wait()
     torch.cuda.synchronize(device)
-    native.check(lib.mg_enable_timing(vec.handle, args.steps))
+    if chunks > 1:
+        vec.enable_timing(args.steps)
+    else:
+        native.check(lib.mg_enable_timing(vec.handle, args.steps))
     if gather:
         shard.enable_restack_timing()
     if world > 1:
@@ -324,15 +339,22 @@ def main():
         step(actions)
     if gather:   # the timed region ends after the last step's exchange (all-gather + restack)
         shard.wait_all()
+    if chunks > 1:   # ... and after every chunk's last step
+        vec.wait()
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     import ctypes
-    tm = (ctypes.c_double * 4)()
-    native.check(lib.mg_read_timing(vec.handle, tm))
+    if chunks > 1:   # per-launch averages over the chunks' launches (each launch covers n / chunks envs)
+        tms = vec.read_timing()
+        tm = [sum(t[i] for t in tms) / chunks for i in range(4)]
+    else:
+        tm = (ctypes.c_double * 4)()
+        native.check(lib.mg_read_timing(vec.handle, tm))
     t_step_ms, t_render_ms, n_timed = tm[0] / args.steps, tm[1] / args.steps, int(tm[2])
     t_reset_ms = tm[3] / args.steps
+    units = n // chunks   # envs one kernel launch completes
     errors = int((vec.errors() != 0).sum().item())
     ranks_seen = world
     if world > 1:
@@ -347,9 +369,10 @@ def main():
     if rank == 0:
         frames_only = gather and args.gather_mode == "frames"
         kernels = {
-            "render_kernel": kernel_record("render_kernel", t_render_ms, spec.preproc, n,
-                                           load_pmc("render_kernel", args.env, n), frames_only),
-            "step_kernel": kernel_record("step_kernel", t_step_ms, spec.preproc, n, load_pmc("step_kernel", args.env, n)),
+            "render_kernel": kernel_record("render_kernel", t_render_ms, spec.preproc, units,
+                                           load_pmc("render_kernel", args.env, units), frames_only),
+            "step_kernel": kernel_record("step_kernel", t_step_ms, spec.preproc, units,
+                                         load_pmc("step_kernel", args.env, units)),
             "reset_kernel": {"ms": round(t_reset_ms, 4)},
         }
         dom = "render_kernel" if t_render_ms >= t_step_ms else "step_kernel"
@@ -372,6 +395,7 @@ def main():
             "config": {"workload": args.env, "envs_per_gpu": n, "episode_steps": spec.max_episode_steps,
                        "physics_substeps": 10, "solver_iterations": 10, "render": "2 x 384^2 -> 96^2",
                        "phase_spread": phase_spread,
+                       "pipeline_chunks": chunks,
                        "parallelism": (f"dp{world} (envs sharded; one packed all-gather per step ({args.gather_mode}), "
                                        f"pipelined with the next step)" if gather else
                                        f"dp{world} (envs sharded, no data-path collective)")},
@@ -383,7 +407,7 @@ def main():
                          "unit": "GB/s", "frac": dk["hbm_frac"], "traffic": dk["traffic_bytes_per_launch"],
                          "traffic_ratio": dk["traffic_ratio"],
                          "traffic_ratio_basis_bytes_per_env_step": dk["traffic_ratio_basis_bytes_per_env_step"],
-                         "bytes_per_env_step": dk["bytes_per_env_step"], "units_per_launch": n,
+                         "bytes_per_env_step": dk["bytes_per_env_step"], "units_per_launch": units,
                          "kernel_avg_ms": dk["ms"],
                          "kernel_bytes": {"bytes_per_env_step": dk["kernel_bytes_per_env_step"],
                                           "achieved": dk["kernel_bytes_achieved_gbs"],
@@ -391,8 +415,11 @@ def main():
                          "binding": "valu_issue_latency",
                          "valu_issue_frac": dk["valu_issue_frac"], "wait_any_frac": dk["wait_any_frac"]},
             "kernels": kernels,
+            # per launch (one launch per chunk and step: chunks > 1 overlap them, so these do not add up to
+            # ms_per_step)
             "kernel_ms_per_step": {"step_kernel": round(t_step_ms, 4), "reset_kernel": round(t_reset_ms, 4),
-                                   "render_kernel": round(t_render_ms, 4), "timed_launches": n_timed},
+                                   "render_kernel": round(t_render_ms, 4), "timed_launches": n_timed,
+                                   "envs_per_launch": units},
             "env_errors": errors,
             "gather": ({"mode": args.gather_mode, "ranks": shard.world, "bytes_per_rank_step": shard.layout.nbytes,
                         "stacked_bytes_per_rank_step": shard.stacked_nbytes,

@@ -127,18 +127,26 @@ __global__ __launch_bounds__(256) void replay_assemble_kernel(const uint8_t *__r
 // The ring view of the stack keeps the env's last 4 frames (slot t % 4 = this step); a fresh env (reset,
 // or done = auto-reset) fills every slot with its current frame, as the deques of
 // benchmarks/__init__.py:75-82,139-147 are filled at reset.  Byte work: per env and stack 12 B read (+ 36 B
-// of ring unless fresh), 12 B ring write and 48 B stacked output per 4 pixels -- HBM bound.  (A 16-pixel
-// form with 16-byte accesses measured 5x slower, round 4: each store instruction then writes 16 B into 64
-// different cache lines, 192 B apart; here 3 back-to-back stores complete the lines.)
+// of ring unless fresh), 12 B ring write and 48 B stacked output per 4 pixels -- HBM bound.
+// The 48 output bytes of a thread's 4 pixels go through LDS (LDSST, the default): the workgroup's 256
+// threads cover 1024 consecutive pixels of one env (a frame is 9 x 1024 pixels), so its stacked output is
+// 12 KB of contiguous memory, stored as 3 fully coalesced 16-byte-per-lane rounds instead of 3 stores of
+// 16 B at a 48 B lane stride.  (A 16-pixel form with 16-byte accesses measured 5x slower, round 4: each
+// store instruction then writes 16 B into 64 different cache lines, 192 B apart.)
+template <bool LDSST>
 __global__ __launch_bounds__(256) void restack_kernel(const uint8_t *__restrict__ recv, uint32_t world, uint32_t n,
                                                       int64_t stride, int64_t off_a, int64_t off_e, int64_t off_d,
                                                       int32_t preproc, uint32_t slot, int32_t all_fresh,
                                                       uint8_t *__restrict__ ring, uint8_t *__restrict__ out0,
                                                       uint8_t *__restrict__ out1) {
     constexpr uint32_t Q = LO * LO / 4;
+    static_assert(Q % 256 == 0, "a workgroup's 256 pixel quads stay inside one env");
+    __shared__ uint4 st[LDSST ? 3 * 256 : 1];
     const uint32_t W = world * n;
     const int s = blockIdx.y;
-    // grid-stride (a capped grid leaves the SIMDs' register files to the simulator's kernels, MG_RESTACK_WGS)
+    uint8_t *const out = s ? out1 : out0;
+    // grid-stride (a capped grid leaves the SIMDs' register files to the simulator's kernels, MG_RESTACK_WGS);
+    // W * Q is a multiple of 256, so every thread of a workgroup runs the same trips
     for (uint32_t gid = blockIdx.x * 256u + threadIdx.x; gid < W * Q; gid += gridDim.x * 256u) {
         const uint32_t g = gid / Q, q = gid - g * Q;
         const uint32_t r = g / n, i = g - r * n;
@@ -178,7 +186,21 @@ __global__ __launch_bounds__(256) void restack_kernel(const uint8_t *__restrict_
 #pragma unroll
             for (int w = 0; w < 3; w++) f[0][w] = a[w];
         }
-        stack_regs(f, (s ? out1 : out0) + (size_t)g * LOFR * 4 + po * 4);
+        if constexpr (LDSST) {
+            uint4 d[3];
+            stack_pack(f, d);
+            const uint32_t t = threadIdx.x;
+#pragma unroll
+            for (int k = 0; k < 3; k++) st[3 * t + k] = d[k];
+            __syncthreads();
+            // the workgroup's quads q0 .. q0 + 255 of env g: 12 KB of output from q0 * 48 on
+            uint4 *dst = (uint4 *)(out + (size_t)g * LOFR * 4 + (size_t)(q - t) * 48);
+#pragma unroll
+            for (int k = 0; k < 3; k++) dst[t + 256 * k] = st[t + 256 * k];
+            __syncthreads();
+        } else {
+            stack_regs(f, out + (size_t)g * LOFR * 4 + po * 4);
+        }
     }
 }
 }  // namespace
@@ -208,8 +230,9 @@ extern "C" hipError_t mg_launch_restack(const uint8_t *recv, int32_t world, int3
     int64_t wgs = (t + 255) / 256;
     static const int64_t cap = getenv("MG_RESTACK_WGS") ? atoll(getenv("MG_RESTACK_WGS")) : 0;   // experiments
     if (cap > 0 && wgs > cap) wgs = cap;
-    hipLaunchKernelGGL(restack_kernel, dim3((unsigned)wgs, two ? 2 : 1), dim3(256), 0, st, recv,
-                       (uint32_t)world, (uint32_t)n, stride, off_a, off_e, off_d, preproc, (uint32_t)(step & 3),
-                       all_fresh, ring, two ? out_allo : out_past, out_ego);
+    static const bool lds = !getenv("MG_RESTACK_LDS") || atoi(getenv("MG_RESTACK_LDS")) != 0;   // A/B
+    hipLaunchKernelGGL(lds ? restack_kernel<true> : restack_kernel<false>, dim3((unsigned)wgs, two ? 2 : 1),
+                       dim3(256), 0, st, recv, (uint32_t)world, (uint32_t)n, stride, off_a, off_e, off_d, preproc,
+                       (uint32_t)(step & 3), all_fresh, ring, two ? out_allo : out_past, out_ego);
     return hipGetLastError();
 }

@@ -1,0 +1,164 @@
+"""Pipelined env pool: one batch of envs as C simulators on C HIP streams.
+
+Why: the robot scenes' step kernel holds a whole CU's LDS per workgroup (16 envs x ~9.8 KB) and runs one
+wavefront per CU for ~0.54 ms whatever the env count, and the render kernel fills the CUs with 16 KB
+workgroups after it; in one stream the two alternate and neither fills the chip.  Split into C chunks, each
+with its own stream, chunk k's render runs beside chunk k+1's step kernel and the next step of chunk 0
+starts as soon as chunk 0's own render is done (round 4, `tools/overlap_ab.py`: MoveToRegion 4096 envs
+2.54 M -> 2.79 M env-steps/s at C = 2, MoveToCorner 1.94 -> 2.08 M; the cooperative many-block scenes are
+slower chunked, ClusterColour 1.48 -> 1.23 M, and keep C = 1).
+
+Semantics: every env is exactly the env of the unchunked `VecMagicalEnv` with the same seed (env i of the
+pool is env i mod m of chunk i // m, seeded as global env i), stepped with its own action in the same order,
+so observations are bit-identical (`tests/test_gpu_parity.py::test_pipelined_pool_matches_batch`).  What
+changes is completion: `step()` only enqueues; a chunk's outputs (views into the pool's full-batch tensors)
+are complete once `wait(k)` / `wait()` has ordered the caller's stream after it -- the asynchronous env-pool
+contract (as EnvPool's async mode), not gym's synchronous one.  Actions are double-buffered on the device,
+so the caller may overwrite its action tensor right after `step()` returns.
+"""
+import collections
+import ctypes
+
+import torch
+
+from . import native
+from .envs import VecMagicalEnv
+
+
+# tasks measured faster pipelined (round 4): their scenes run the compile-time robot forms of the step
+# kernel (16 envs per workgroup: one workgroup per CU at 4096 envs, the CU's whole LDS)
+PIPELINED_TASKS = ("MoveToRegion", "MoveToCorner")
+
+
+def default_chunks(spec, num_envs):
+    """bench.py --chunks auto: 2 for the robot scenes at >= 2048 envs, else 1."""
+    return 2 if spec.task in PIPELINED_TASKS and num_envs >= 2048 and num_envs % 2 == 0 else 1
+
+
+class PipelinedVecEnv:
+    def __init__(self, env_name, num_envs, chunks=2, device="cuda:0", seeds=None, base_seed=0, **kw):
+        num_envs, chunks = int(num_envs), int(chunks)
+        if chunks < 1 or num_envs % chunks:
+            raise ValueError(f"PipelinedVecEnv: {num_envs} envs do not split into {chunks} equal chunks")
+        self.num_envs, self.chunks, self.m = num_envs, chunks, num_envs // chunks
+        self.device = torch.device(device)
+        seeds = list(seeds) if seeds is not None else [base_seed + i for i in range(num_envs)]
+        if len(seeds) != num_envs:
+            raise ValueError("PipelinedVecEnv: one seed per env")
+        m = self.m
+        self.sims = [VecMagicalEnv(env_name, m, device=device, seeds=seeds[k * m:(k + 1) * m], **kw)
+                     for k in range(chunks)]
+        s0 = self.sims[0]
+        self.spec, self.lib, self.max_episode_steps = s0.spec, s0.lib, s0.max_episode_steps
+        self.action_space, self.observation_space = s0.action_space, s0.observation_space
+        if self.spec.preproc is None:
+            raise ValueError("PipelinedVecEnv: LoRes preprocessors only (the 384^2 view is rendered on demand)")
+        # the pool's full-batch outputs; chunk k writes rows [k*m, (k+1)*m)
+        self.buffers = collections.OrderedDict(
+            (k, torch.empty((num_envs,) + tuple(v.shape[1:]), dtype=v.dtype, device=self.device))
+            for k, v in s0.output_buffers().items() if k != "target")
+        for k, sim in enumerate(self.sims):
+            sim.bind_outputs({key: buf[k * m:(k + 1) * m] for key, buf in self.buffers.items()})
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(chunks)]
+        self.abuf = torch.zeros((2, num_envs), dtype=torch.uint8, device=self.device)
+        # done[k][slot]: chunk k finished the step that read action slot `slot`
+        self.done_ev = [[None, None] for _ in range(chunks)]
+        self.t = 0
+
+    # -- ordering ------------------------------------------------------------------
+    def _caller(self):
+        return torch.cuda.current_stream(self.device)
+
+    def _fork(self):
+        """The chunk streams wait for the caller's work so far."""
+        ev = torch.cuda.Event()
+        ev.record(self._caller())
+        for st in self.streams:
+            st.wait_event(ev)
+
+    def wait(self, chunk=None):
+        """Order the caller's stream after chunk `chunk` (all chunks when None): its outputs are then complete."""
+        cs = self._caller()
+        for k in (range(self.chunks) if chunk is None else [chunk]):
+            ev = torch.cuda.Event()
+            ev.record(self.streams[k])
+            cs.wait_event(ev)
+
+    # -- API -----------------------------------------------------------------------
+    def reset(self, mask=None):
+        self.wait()
+        for k, sim in enumerate(self.sims):
+            sim.reset(None if mask is None else mask[k * self.m:(k + 1) * self.m])
+        self._fork()
+        return self._obs()
+
+    def step(self, actions):
+        a = actions
+        if not (isinstance(a, torch.Tensor) and a.dtype == torch.uint8 and a.device == self.device):
+            a = torch.as_tensor(actions).to(self.device, torch.uint8)
+        slot = self.t & 1
+        cs = self._caller()
+        for k in range(self.chunks):   # the step two calls ago has read this slot
+            if self.done_ev[k][slot] is not None:
+                cs.wait_event(self.done_ev[k][slot])
+        self.abuf[slot].copy_(a)
+        self._fork()
+        m = self.m
+        for k, (sim, st) in enumerate(zip(self.sims, self.streams)):
+            with torch.cuda.stream(st):
+                sim.step(self.abuf[slot, k * m:(k + 1) * m])
+            ev = torch.cuda.Event()
+            ev.record(st)
+            self.done_ev[k][slot] = ev
+        self.t += 1
+        return self._obs(), self.buffers["reward"], self.buffers["done"], {"eval_score": self.buffers["eval_score"]}
+
+    def _obs(self):
+        out = collections.OrderedDict([("allo", self.buffers["allo"]), ("ego", self.buffers["ego"])])
+        if self.sims[0]._chw:
+            out = collections.OrderedDict((k, v.permute(0, 3, 1, 2)) for k, v in out.items())
+        if self.sims[0].target is not None:
+            t = torch.cat([s.target for s in self.sims]).to(torch.float32)
+            out["target_type"], out["target_colour"], out["target_position"] = t[:, 0:1], t[:, 1:2], t[:, 2:4]
+        if "past_obs" in self.buffers:
+            p = self.buffers["past_obs"]
+            out["past_obs"] = p.permute(0, 3, 1, 2) if self.sims[0]._chw else p
+        return out
+
+    def random_actions(self, step, key=42, out=None):
+        """Device Philox actions for a random policy (chunk k draws with key + k)."""
+        out = out if out is not None else torch.empty(self.num_envs, dtype=torch.uint8, device=self.device)
+        m = self.m
+        for k, sim in enumerate(self.sims):
+            sim.random_actions(step, key=key + k, out=out[k * m:(k + 1) * m])
+        return out
+
+    def set_episode_steps(self, steps):
+        self.wait()
+        s = torch.as_tensor(steps)
+        for k, sim in enumerate(self.sims):
+            sim.set_episode_steps(s[k * self.m:(k + 1) * self.m])
+        self._fork()
+
+    def errors(self):
+        self.wait()
+        return torch.cat([sim.errors() for sim in self.sims])
+
+    def enable_timing(self, steps):
+        """Per-chunk HIP-event timing of the kernels (mg_enable_timing on every chunk's simulator)."""
+        self.wait()
+        for sim in self.sims:
+            native.check(self.lib.mg_enable_timing(sim.handle, int(steps)))
+
+    def read_timing(self):
+        """[chunks][4] totals over the timed launches (mg_read_timing: step ms, render ms, launches, reset ms)."""
+        out = []
+        for sim in self.sims:
+            tm = (ctypes.c_double * 4)()
+            native.check(self.lib.mg_read_timing(sim.handle, tm))
+            out.append(list(tm))
+        return out
+
+    def close(self):
+        for sim in self.sims:
+            sim.close()

@@ -864,3 +864,36 @@ def test_single_env_reset_after_placement_error(monkeypatch, name):
         for key in want:
             assert np.array_equal(obs[key], want[key]), (k, key)
     env.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n,chunks,L", [("MoveToRegion-Demo-LoRes4E-v0", 256, 2, 40),
+                                             ("MoveToCorner-Demo-LoRes4E-v0", 96, 3, 25),
+                                             ("ClusterColour-Demo-LoResStack-v0", 64, 4, 20)])
+def test_pipelined_pool_matches_batch(name, n, chunks, L):
+    """magical_amd.pipeline: C simulators on C streams (env i of the pool seeded as env i of the batch) give the
+    batch's outputs bit for bit, across episode boundaries, with the caller's action tensor overwritten right
+    after every step() (the pool double-buffers actions on the device)."""
+    from magical_amd import pipeline
+    seeds = [1000 + i for i in range(n)]
+    ref = mg_envs.VecMagicalEnv(name, n, seeds=seeds, max_episode_steps=L)
+    pool = pipeline.PipelinedVecEnv(name, n, chunks=chunks, seeds=seeds, max_episode_steps=L)
+    o_ref, o_pool = ref.reset(), pool.reset()
+    pool.wait()
+    for k in o_ref:
+        assert torch.equal(o_ref[k], o_pool[k]), k
+    acts = np.random.RandomState(42).randint(0, 18, (2 * L + 5, n)).astype(np.uint8)
+    a_dev = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    for t in range(acts.shape[0]):
+        a_dev.copy_(torch.from_numpy(acts[t]))
+        o_ref, r_ref, d_ref, i_ref = ref.step(a_dev)
+        o_pool, r_pool, d_pool, i_pool = pool.step(a_dev)
+        a_dev.fill_(255)   # the pool must not read the caller's tensor after step() returns
+        pool.wait()
+        for k in o_ref:
+            assert torch.equal(o_ref[k], o_pool[k]), (k, t)
+        assert torch.equal(r_ref, r_pool) and torch.equal(d_ref, d_pool), t
+        assert torch.equal(i_ref["eval_score"], i_pool["eval_score"]), t
+    assert int((pool.errors() != 0).sum()) == 0
+    pool.close()
+    ref.close()

@@ -574,3 +574,13 @@ def test_latexify_results_matches_reference():
     with pytest.raises(ValueError) as ei:
         evaluation.latexify_results(pd.DataFrame.from_records(ref["duplicate"]["records"]))
     assert str(ei.value) == ref["duplicate"]["error"]
+
+
+def test_pipeline_default_chunks():
+    """bench.py --chunks auto: the robot scenes pipeline 2 chunks at >= 2048 envs, every other scene runs 1."""
+    from magical_amd import pipeline
+    assert pipeline.default_chunks(registry.lookup("MoveToRegion-Demo-LoRes4E-v0"), 4096) == 2
+    assert pipeline.default_chunks(registry.lookup("MoveToCorner-Demo-LoRes4E-v0"), 4096) == 2
+    assert pipeline.default_chunks(registry.lookup("MoveToRegion-Demo-LoRes4E-v0"), 64) == 1
+    assert pipeline.default_chunks(registry.lookup("ClusterColour-Demo-LoResStack-v0"), 8192) == 1
+    assert pipeline.default_chunks(registry.lookup("MatchRegions-TestAll-LoRes4E-v0"), 8192) == 1
