@@ -150,7 +150,8 @@ def load_pmc(kernel, workload, envs):
     """PMC record of `kernel` (HBM bytes per launch, VALU issue fraction) from the committed passes, newest
     first: profiles/r02_final/<workload>.traffic.json (tools/gpu_table.sh at the round's final build), then
     profiles/r02_table/, then profiles/pmc_traffic.json -- only when collected on this workload and env count."""
-    for path in (os.path.join(ROOT, "profiles", "r03_final", f"{workload}.traffic.json"),
+    for path in (os.path.join(ROOT, "profiles", "r04_final", f"{workload}.traffic.json"),
+                 os.path.join(ROOT, "profiles", "r03_final", f"{workload}.traffic.json"),
                  os.path.join(ROOT, "profiles", "r02_final", f"{workload}.traffic.json"),
                  os.path.join(ROOT, "profiles", "r02_table", f"{workload}.traffic.json"),
                  os.path.join(ROOT, "profiles", "pmc_traffic.json")):
@@ -354,7 +355,15 @@ def main():
         native.check(lib.mg_read_timing(vec.handle, tm))
     t_step_ms, t_render_ms, n_timed = tm[0] / args.steps, tm[1] / args.steps, int(tm[2])
     t_reset_ms = tm[3] / args.steps
-    units = n // chunks   # envs one kernel launch completes
+    units = n / chunks   # envs one kernel launch completes (on average over the chunks)
+
+    def pmc_for(kernel):
+        """The committed PMC record of this workload; the passes run unchunked (n envs per launch), so a
+        chunked line scales its bytes per launch to the chunk's envs."""
+        rec = load_pmc(kernel, args.env, n)
+        if rec and chunks > 1 and rec.get("bytes_per_launch"):
+            rec = dict(rec, bytes_per_launch=rec["bytes_per_launch"] * units / n, scaled_from_envs=n)
+        return rec
     errors = int((vec.errors() != 0).sum().item())
     ranks_seen = world
     if world > 1:
@@ -370,9 +379,8 @@ def main():
         frames_only = gather and args.gather_mode == "frames"
         kernels = {
             "render_kernel": kernel_record("render_kernel", t_render_ms, spec.preproc, units,
-                                           load_pmc("render_kernel", args.env, units), frames_only),
-            "step_kernel": kernel_record("step_kernel", t_step_ms, spec.preproc, units,
-                                         load_pmc("step_kernel", args.env, units)),
+                                           pmc_for("render_kernel"), frames_only),
+            "step_kernel": kernel_record("step_kernel", t_step_ms, spec.preproc, units, pmc_for("step_kernel")),
             "reset_kernel": {"ms": round(t_reset_ms, 4)},
         }
         dom = "render_kernel" if t_render_ms >= t_step_ms else "step_kernel"
@@ -407,7 +415,7 @@ def main():
                          "unit": "GB/s", "frac": dk["hbm_frac"], "traffic": dk["traffic_bytes_per_launch"],
                          "traffic_ratio": dk["traffic_ratio"],
                          "traffic_ratio_basis_bytes_per_env_step": dk["traffic_ratio_basis_bytes_per_env_step"],
-                         "bytes_per_env_step": dk["bytes_per_env_step"], "units_per_launch": units,
+                         "bytes_per_env_step": dk["bytes_per_env_step"], "units_per_launch": round(units, 1),
                          "kernel_avg_ms": dk["ms"],
                          "kernel_bytes": {"bytes_per_env_step": dk["kernel_bytes_per_env_step"],
                                           "achieved": dk["kernel_bytes_achieved_gbs"],
@@ -419,7 +427,7 @@ def main():
             # ms_per_step)
             "kernel_ms_per_step": {"step_kernel": round(t_step_ms, 4), "reset_kernel": round(t_reset_ms, 4),
                                    "render_kernel": round(t_render_ms, 4), "timed_launches": n_timed,
-                                   "envs_per_launch": units},
+                                   "envs_per_launch": round(units, 1)},
             "env_errors": errors,
             "gather": ({"mode": args.gather_mode, "ranks": shard.world, "bytes_per_rank_step": shard.layout.nbytes,
                         "stacked_bytes_per_rank_step": shard.stacked_nbytes,

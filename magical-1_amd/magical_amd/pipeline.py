@@ -10,7 +10,9 @@ slower chunked, ClusterColour 1.48 -> 1.23 M, and keep C = 1).
 
 Semantics: every env is exactly the env of the unchunked `VecMagicalEnv` with the same seed (env i of the
 pool is env i mod m of chunk i // m, seeded as global env i), stepped with its own action in the same order,
-so observations are bit-identical (`tests/test_gpu_parity.py::test_pipelined_pool_matches_batch`).  What
+so observations are bit-identical (`tests/test_gpu_parity.py::test_pipelined_pool_matches_batch`).  Chunks
+are equal shares of the envs rounded to the step kernel's 16-env workgroups; at most 3, since a process has
+4 hardware queues (GPU_MAX_HW_QUEUES) and the caller's stream takes one.  What
 changes is completion: `step()` only enqueues; a chunk's outputs (views into the pool's full-batch tensors)
 are complete once `wait(k)` / `wait()` has ordered the caller's stream after it -- the asynchronous env-pool
 contract (as EnvPool's async mode), not gym's synchronous one.  Actions are double-buffered on the device,
@@ -38,27 +40,31 @@ def default_chunks(spec, num_envs):
 class PipelinedVecEnv:
     def __init__(self, env_name, num_envs, chunks=2, device="cuda:0", seeds=None, base_seed=0, **kw):
         num_envs, chunks = int(num_envs), int(chunks)
-        if chunks < 1 or num_envs % chunks:
-            raise ValueError(f"PipelinedVecEnv: {num_envs} envs do not split into {chunks} equal chunks")
-        self.num_envs, self.chunks, self.m = num_envs, chunks, num_envs // chunks
+        if chunks < 1 or chunks > min(num_envs, 3):
+            raise ValueError(f"PipelinedVecEnv: {num_envs} envs do not split into {chunks} chunks")
+        self.num_envs, self.chunks = num_envs, chunks
+        # chunk bounds: equal shares rounded to the step kernel's 16-env workgroups where the count allows
+        q = 16 if num_envs >= 16 * chunks else 1
+        units = num_envs // q
+        self.bounds = [q * (units * k // chunks) for k in range(chunks)] + [num_envs]
         self.device = torch.device(device)
         seeds = list(seeds) if seeds is not None else [base_seed + i for i in range(num_envs)]
         if len(seeds) != num_envs:
             raise ValueError("PipelinedVecEnv: one seed per env")
-        m = self.m
-        self.sims = [VecMagicalEnv(env_name, m, device=device, seeds=seeds[k * m:(k + 1) * m], **kw)
+        b = self.bounds
+        self.sims = [VecMagicalEnv(env_name, b[k + 1] - b[k], device=device, seeds=seeds[b[k]:b[k + 1]], **kw)
                      for k in range(chunks)]
         s0 = self.sims[0]
         self.spec, self.lib, self.max_episode_steps = s0.spec, s0.lib, s0.max_episode_steps
         self.action_space, self.observation_space = s0.action_space, s0.observation_space
         if self.spec.preproc is None:
             raise ValueError("PipelinedVecEnv: LoRes preprocessors only (the 384^2 view is rendered on demand)")
-        # the pool's full-batch outputs; chunk k writes rows [k*m, (k+1)*m)
+        # the pool's full-batch outputs; chunk k writes rows [bounds[k], bounds[k + 1])
         self.buffers = collections.OrderedDict(
             (k, torch.empty((num_envs,) + tuple(v.shape[1:]), dtype=v.dtype, device=self.device))
             for k, v in s0.output_buffers().items() if k != "target")
         for k, sim in enumerate(self.sims):
-            sim.bind_outputs({key: buf[k * m:(k + 1) * m] for key, buf in self.buffers.items()})
+            sim.bind_outputs({key: buf[b[k]:b[k + 1]] for key, buf in self.buffers.items()})
         self.streams = [torch.cuda.Stream(self.device) for _ in range(chunks)]
         self.abuf = torch.zeros((2, num_envs), dtype=torch.uint8, device=self.device)
         # done[k][slot]: chunk k finished the step that read action slot `slot`
@@ -88,7 +94,7 @@ class PipelinedVecEnv:
     def reset(self, mask=None):
         self.wait()
         for k, sim in enumerate(self.sims):
-            sim.reset(None if mask is None else mask[k * self.m:(k + 1) * self.m])
+            sim.reset(None if mask is None else mask[self.bounds[k]:self.bounds[k + 1]])
         self._fork()
         return self._obs()
 
@@ -103,10 +109,10 @@ class PipelinedVecEnv:
                 cs.wait_event(self.done_ev[k][slot])
         self.abuf[slot].copy_(a)
         self._fork()
-        m = self.m
+        b = self.bounds
         for k, (sim, st) in enumerate(zip(self.sims, self.streams)):
             with torch.cuda.stream(st):
-                sim.step(self.abuf[slot, k * m:(k + 1) * m])
+                sim.step(self.abuf[slot, b[k]:b[k + 1]])
             ev = torch.cuda.Event()
             ev.record(st)
             self.done_ev[k][slot] = ev
@@ -128,16 +134,16 @@ class PipelinedVecEnv:
     def random_actions(self, step, key=42, out=None):
         """Device Philox actions for a random policy (chunk k draws with key + k)."""
         out = out if out is not None else torch.empty(self.num_envs, dtype=torch.uint8, device=self.device)
-        m = self.m
+        b = self.bounds
         for k, sim in enumerate(self.sims):
-            sim.random_actions(step, key=key + k, out=out[k * m:(k + 1) * m])
+            sim.random_actions(step, key=key + k, out=out[b[k]:b[k + 1]])
         return out
 
     def set_episode_steps(self, steps):
         self.wait()
         s = torch.as_tensor(steps)
         for k, sim in enumerate(self.sims):
-            sim.set_episode_steps(s[k * self.m:(k + 1) * self.m])
+            sim.set_episode_steps(s[self.bounds[k]:self.bounds[k + 1]])
         self._fork()
 
     def errors(self):

@@ -869,7 +869,7 @@ def test_single_env_reset_after_placement_error(monkeypatch, name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,n,chunks,L", [("MoveToRegion-Demo-LoRes4E-v0", 256, 2, 40),
                                              ("MoveToCorner-Demo-LoRes4E-v0", 96, 3, 25),
-                                             ("ClusterColour-Demo-LoResStack-v0", 64, 4, 20)])
+                                             ("ClusterColour-Demo-LoResStack-v0", 64, 3, 20)])
 def test_pipelined_pool_matches_batch(name, n, chunks, L):
     """magical_amd.pipeline: C simulators on C streams (env i of the pool seeded as env i of the batch) give the
     batch's outputs bit for bit, across episode boundaries, with the caller's action tensor overwritten right

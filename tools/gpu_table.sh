@@ -1,7 +1,9 @@
 #!/bin/bash
 # BASELINE.md results table: every BASELINE config on one GPU with its CPU-restatement baseline
 # (1 process, then 16 processes = the job's CPU share), a kernel-trace stats pass and the PMC passes
-# (FETCH_SIZE, WRITE_SIZE, SQ) of each config, summarised on the box (the rocpd databases are dropped:
+# (FETCH_SIZE, WRITE_SIZE, SQ) of each config, summarised on the box (the stats pass runs the bench line's own
+# default, pipelined chunks included; the PMC passes run unchunked, --chunks 1, so that each launch covers
+# all envs and its counters are not mixed with a concurrent kernel's) (the rocpd databases are dropped:
 # gpurun copies back at most 64 MiB).  Output: gpurun_out/table/<config>.{json,log,md,traffic.json}.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out/table
 export PYTHONDONTWRITEBYTECODE=1
@@ -14,9 +16,9 @@ for spec in "MoveToRegion-Demo-LoRes4E-v0 4096" "MoveToCorner-Demo-LoRes4E-v0 40
   cd /tmp && export TMPDIR=/tmp
   B="--env $1 --envs $2 --no-cpu-baseline"
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$T.prof/stats" -o run -- python "$R/bench.py" $B --steps 20 --warmup 5 > /dev/null 2>&1 || { echo "FAIL stats $1"; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$T.prof/fetch" -o run -- python "$R/bench.py" $B --steps 5 --warmup 2 > /dev/null 2>&1 || { echo "FAIL fetch $1"; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$T.prof/write" -o run -- python "$R/bench.py" $B --steps 5 --warmup 2 > /dev/null 2>&1 || { echo "FAIL write $1"; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$T.prof/sq" -o run -- python "$R/bench.py" $B --steps 5 --warmup 2 > /dev/null 2>&1 || { echo "FAIL sq $1"; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$T.prof/fetch" -o run -- python "$R/bench.py" $B --chunks 1 --steps 5 --warmup 2 > /dev/null 2>&1 || { echo "FAIL fetch $1"; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$T.prof/write" -o run -- python "$R/bench.py" $B --chunks 1 --steps 5 --warmup 2 > /dev/null 2>&1 || { echo "FAIL write $1"; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$T.prof/sq" -o run -- python "$R/bench.py" $B --chunks 1 --steps 5 --warmup 2 > /dev/null 2>&1 || { echo "FAIL sq $1"; exit 1; }
   cd "$R"
   python tools/prof_summary.py "$T.prof" --md > $T.md || exit 1
   for k in render_kernel step_kernel reset_kernel; do
