@@ -16,10 +16,12 @@ struct RenderOut {
     int frames_only;      // 1: obs_allo / obs_ego get the current [N][96][96][3] frames only (no stacks, no ring)
     int debug_skip;      // profiling builds only: 1 skip outlines, 2 skip fill, 4 skip HBM stores, 8 skip spans
     int small;            // 1: robot + arena + goal + one block at most (MoveToRegion, MoveToCorner) -> small LDS class
-    int retry_in;         // set by mg_launch_render: render only the (env, view) pairs marked in S.rg_retry
-    int retry_out;        // ... a pair this class cannot hold is marked for the next class (else an env error)
+    int retry_in;         // set by mg_launch_render: class chain, render only the pairs at this class's level
+                          // (S.rg_retry: the level that holds each (env, view) this episode)
+    int retry_out;        // ... a pair this class cannot hold moves to the next level (else an env error)
     int cls_level;        // ... position of this class in the chain
-    int force_retry;      // tests: classes below this level mark every pair (1: skip the first, 2: the first two)
+    int first_level;      // ... the chain's first class for this task (0: medium-0, 1: medium-1)
+    int force_retry;      // tests: classes below this level hand every pair on (1: skip the first, 2: the first two)
     int scache_mode;      // tests / A-B (MG_DEBUG_SCACHE): 1 = no allocentric static layer, 2 = its copied blocks
                           // poisoned (0x55) -- shows where the layer is used
 };

@@ -11,21 +11,33 @@ hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderO
         else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_SMALL>, 1>), grid, blk, 0, st, S, L, r);
         return hipGetLastError();
     }
-    // many-block tasks: a chain of classes, each with more LDS (fewer workgroups per CU) than the last;
-    // the (env, view) pairs a class cannot hold are marked and rendered by the next one (the others exit
-    // at once).  Medium-1 (7 workgroups/CU) holds most scenes of the benchmark tasks, medium-2 (5) nearly
-    // all, the large class (3) every scene.
-    r.retry_out = 1;
+    // many-block tasks: a chain of classes, each with more LDS (fewer workgroups per CU) than the last.  A
+    // class renders the (env, view) pairs at its chain level (S.rg_retry, kept for the episode); a pair it
+    // cannot hold moves to the next level and is rendered by the next class (the others exit at once).
+    // Medium-0 (8 workgroups/CU) holds every ClusterColour scene, medium-1 (7) most scenes of the other
+    // benchmark tasks, medium-2 (5) nearly all, the large class (3) every scene.
+    // Where the chain starts is the task's (first_level): medium-0 holds every ClusterColour scene, but a third
+    // of MatchRegions-TestAll's, whose frames then pay a launch more and measured slower (3.30 -> 3.59 ms), so
+    // the other tasks start at medium-1.
+    r.retry_in = 1; r.retry_out = 1;
+    hipError_t e;
+    if (r.first_level == 0) {
+        if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM0>, 0>), grid, blk, 0, st, S, L, r);
+        else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM0>, 1>), grid, blk, 0, st, S, L, r);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    r.cls_level = 1;
     if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM1>, 0>), grid, blk, 0, st, S, L, r);
     else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM1>, 1>), grid, blk, 0, st, S, L, r);
-    hipError_t e = hipGetLastError();
+    e = hipGetLastError();
     if (e != hipSuccess) return e;
-    r.retry_in = 1; r.cls_level = 1;
+    r.cls_level = 2;
     if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM2>, 0>), grid, blk, 0, st, S, L, r);
     else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM2>, 1>), grid, blk, 0, st, S, L, r);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    r.retry_out = 0; r.cls_level = 2;
+    r.retry_out = 0; r.cls_level = 3;
     if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_LARGE>, 0>), grid, blk, 0, st, S, L, r);
     else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_LARGE>, 1>), grid, blk, 0, st, S, L, r);
     return hipGetLastError();

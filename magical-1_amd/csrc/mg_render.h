@@ -26,6 +26,9 @@
 // per entity).  The large class fits every task; the small one fits robot + arena + goal + one block
 // (MoveToRegion / MoveToCorner) and leaves room for 9 workgroups/CU.
 #define RG_LARGE 160, 1600, 256, 3072, 1600, MG_MAX_ENTS, uint32_t
+#ifndef RG_MEDIUM0
+#define RG_MEDIUM0 44, 784, 128, 1280, 512, MG_MAX_ENTS, uint16_t   // 20.3 KB: 8 workgroups/CU
+#endif
 #ifndef RG_MEDIUM1
 #define RG_MEDIUM1 48, 896, 160, 1536, 512, MG_MAX_ENTS, uint16_t
 #endif
@@ -479,7 +482,17 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     constexpr int mode = MODE;
     const int e = blockIdx.x, view = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
     if (e >= S.n_envs || (out.mask && !out.mask[e])) return;
-    if (out.retry_in && !S.rg_retry[2 * e + view]) return;
+    // class chain (many-block tasks): S.rg_retry[e][view] holds the chain level that holds this (env, view)
+    // in the current episode -- scenes keep their entities for an episode, so a pair that overflowed a class
+    // skips it on later frames instead of rebuilding its setup there first.  An episode's first frame starts
+    // again at the chain's first level.  Each class renders the pairs at its own level only.
+    if (out.retry_in) {
+        const bool restart = out.cls_level == out.first_level && S.episode_steps[e] == 0;
+        const int stored = S.rg_retry[2 * e + view];
+        const int lvl = restart || stored < out.first_level ? out.first_level : stored;
+        if (lvl != out.cls_level) return;
+        if (tid == 0 && stored != lvl) S.rg_retry[2 * e + view] = (uint8_t)lvl;
+    }
     // an episode's first allo frame invalidates the static layer of the previous episode before anything can
     // fail: a frame that a class hands over (or gives up on) must not leave the old layer marked valid
     // (ADVICE r3); a successful first frame of the layer's class sets it again at the end
@@ -487,10 +500,11 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     MG_PROF_BEGIN(tid == 0);
     // capacity overflow: a class with a successor hands the (env, view) to it, else an env error
 #define RG_FAIL() do { \
-        if (tid == 0) { if (out.retry_out) S.rg_retry[2 * e + view] = 1; else S.overflow[e] |= 4 << view; } \
+        if (tid == 0) { if (out.retry_out) S.rg_retry[2 * e + view] = (uint8_t)(out.cls_level + 1); \
+                        else S.overflow[e] |= 4 << view; } \
         return; } while (0)
     const int nents = S.nents[e];
-    if (nents > SM::RG_MAXE || (out.retry_out && out.force_retry > out.cls_level)) RG_FAIL();
+    if (nents > SM::RG_MAXE || (out.retry_out && out.force_retry > out.cls_level - out.first_level)) RG_FAIL();
     // ---- 1. geometry list (entity add order x render polys), colour table, view ----
     int my_r0 = 0, my_nr = 0;
     if (tid < nents) {
@@ -542,7 +556,6 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
 #endif
     RG_SYNC();
     MG_PROF(10);
-    if (out.retry_in && tid == 0) S.rg_retry[2 * e + view] = 0;   // every wave has read it (barrier above)
 #if RG_XF_LATE
     // every thread forms the entities' first-geom offsets itself from the per-entity counts (independent
     // LDS reads, no barrier); the entity transforms and the view matrix (long serial f64 chains, correctly

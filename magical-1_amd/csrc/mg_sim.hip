@@ -286,6 +286,7 @@ static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
     ro.mask = mask;
     ro.debug_skip = 0;
     ro.small = s->task == MG_TASK_MOVE_TO_REGION || s->task == MG_TASK_MOVE_TO_CORNER;
+    ro.first_level = s->task == MG_TASK_CLUSTER_COLOUR ? 0 : 1;   // render class chain start (mg_raster.hip)
     ro.force_retry = s->force_render_retry;
     ro.scache_mode = s->scache_mode;
 #ifdef MG_PROFILE
@@ -547,6 +548,7 @@ int mg_render_full(mg_sim *s, uint8_t *out, void *stream) {
     ro.full = out;
     ro.preproc = s->preproc;
     ro.small = s->task == MG_TASK_MOVE_TO_REGION || s->task == MG_TASK_MOVE_TO_CORNER;
+    ro.first_level = s->task == MG_TASK_CLUSTER_COLOUR ? 0 : 1;   // render class chain start (mg_raster.hip)
     ro.force_retry = s->force_render_retry;
     HIPC(mg_launch_render(s->S, s->dlib, ro, 1, as_stream(stream)));
     return 0;

@@ -42,7 +42,7 @@ struct MGState {
     uint32_t *stamp;
     double *curr_dt;
     int32_t *overflow;       // per env error flags
-    uint8_t *rg_retry;       // [N][2]: (env, view) pairs the medium render class could not hold this step
+    uint8_t *rg_retry;       // [N][2]: render class chain level that holds each (env, view) this episode
     // ---- robot control + physics variables [N] ----
     double *target_speed, *rel_turn, *target_finger;
     int32_t *robot_body0, *robot_cons0;
