@@ -203,6 +203,7 @@ __global__ __launch_bounds__(256) void restack_kernel(const uint8_t *__restrict_
         }
     }
 }
+
 }  // namespace
 
 // launcher, C linkage (declared in mg_sim.hip next to the ABI entry mg_replay_lores)
@@ -230,7 +231,10 @@ extern "C" hipError_t mg_launch_restack(const uint8_t *recv, int32_t world, int3
     int64_t wgs = (t + 255) / 256;
     static const int64_t cap = getenv("MG_RESTACK_WGS") ? atoll(getenv("MG_RESTACK_WGS")) : 0;   // experiments
     if (cap > 0 && wgs > cap) wgs = cap;
-    static const bool lds = !getenv("MG_RESTACK_LDS") || atoi(getenv("MG_RESTACK_LDS")) != 0;   // A/B
+    // A/B: MG_RESTACK_LDS=0 direct 16-byte stores at a 48-byte lane stride.  (A form staging every load
+    // through LDS as well -- 192 lanes x 16 B per frame chunk -- measured no faster, round 4: 2.13 vs 2.06 ms
+    // MoveToRegion, 10.5 vs 9.9 ms ClusterColour at 8 emulated ranks.)
+    static const bool lds = !getenv("MG_RESTACK_LDS") || atoi(getenv("MG_RESTACK_LDS")) != 0;
     hipLaunchKernelGGL(lds ? restack_kernel<true> : restack_kernel<false>, dim3((unsigned)wgs, two ? 2 : 1),
                        dim3(256), 0, st, recv, (uint32_t)world, (uint32_t)n, stride, off_a, off_e, off_d, preproc,
                        (uint32_t)(step & 3), all_fresh, ring, two ? out_allo : out_past, out_ego);
