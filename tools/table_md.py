@@ -26,7 +26,10 @@ def main(d):
         km = b["kernel_ms_per_step"]
         cb = b["cpu_baseline"]
         r = t["render_kernel"]
-        rg = r["bytes_per_launch"] / (km["render_kernel"] * 1e-3) / 1e9
+        # the PMC passes run unchunked (envs per launch = the traffic record's envs); a pipelined bench line's
+        # launches cover envs_per_launch envs each
+        sc = km.get("envs_per_launch", r["envs"]) / r["envs"]
+        rg = r["bytes_per_launch"] * sc / (km["render_kernel"] * 1e-3) / 1e9
         rows.append(f"| {n} | {b['config']['envs_per_gpu']} | 1 | {b['value']:,.0f} | {b['ms_per_step']:.3f} | "
                     f"{b['roofline']['bytes_per_env_step']:,} | {b['roofline']['achieved']:.0f} | {rg:.0f} | "
                     f"{b['roofline']['achieved'] / 8000:.3f} | {r.get('valu_issue_frac', float('nan')):.2f} | "
@@ -36,8 +39,8 @@ def main(d):
                 continue
             v = t[k]
             ms = km.get(k, float("nan"))
-            krows.append(f"| {n} | {k} | {ms:.3f} | {v['read_bytes'] / 1e6:.1f} | {v['write_bytes'] / 1e6:.1f} | "
-                         f"{v['bytes_per_launch'] / (ms * 1e-3) / 1e9:.0f} | {v.get('valu_issue_frac', float('nan')):.3f} | "
+            krows.append(f"| {n} | {k} | {ms:.3f} | {v['read_bytes'] * sc / 1e6:.1f} | {v['write_bytes'] * sc / 1e6:.1f} | "
+                         f"{v['bytes_per_launch'] * sc / (ms * 1e-3) / 1e9:.0f} | {v.get('valu_issue_frac', float('nan')):.3f} | "
                          f"{v.get('wait_any_frac', float('nan')):.3f} | {v['sq'].get('SQ_INSTS_VALU', 0) / max(v['sq'].get('SQ_WAVES', 1), 1):,.0f} |")
     print("| config | envs/GPU | GPUs | env-steps/s | ms/step | algorithmic B/env-step | render GB/s (algorithmic) | "
           "render GB/s (PMC) | HBM fraction (algorithmic / 8 TB/s) | render VALU issue | CPU restatement env-steps/s "
@@ -45,7 +48,7 @@ def main(d):
     print("|---|---|---|---|---|---|---|---|---|---|---|")
     print("\n".join(rows))
     print()
-    print("| config | kernel | ms/launch (HIP events) | PMC read MB | PMC write MB | PMC GB/s | VALU issue frac | "
+    print("| config | kernel | ms/launch (HIP events; per chunk when pipelined) | PMC read MB | PMC write MB | PMC GB/s | VALU issue frac | "
           "wait-any frac | VALU instrs/wave |")
     print("|---|---|---|---|---|---|---|---|---|")
     print("\n".join(krows))
