@@ -421,6 +421,11 @@ __constant__ static const double FC_REGIONS[3][4] = {{-0.032, 0.348, 0.427, 0.46
                                                      {-0.681, 0.196, 0.498, 0.418}};
 __constant__ static const int FC_REGION_COLOURS[3] = {MG_COL_GREEN, MG_COL_GREEN, MG_COL_RED};
 
+// TASK >= 0: a reset kernel compiled for that task alone; LAYOUT == 0: for variants without layout
+// randomisation (flags without MG_RAND_LAYOUT_*) -- the other tasks' and the rejection samplers' code is
+// dropped, so the kernel needs far fewer registers (mg_launch_reset)
+template <int TASK> MG_DEV constexpr bool task_is(int runtime_task, int t) { return TASK >= 0 ? TASK == t : runtime_task == t; }
+template <int TASK = -1, int LAYOUT = -1>
 MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg) {
     size_t N = (size_t)S.N;
     // cooperative reset (reset_kernel_coop): the wave's 64 lanes all run this env's reset with the same
@@ -440,10 +445,10 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
     Builder B = {0, 0, 0, 4}; // arena segments hold hashids 0..3
     new_entity(S, e, MG_ENT_ARENA, 0, MG_COL_GREY, 0, 0, 0, 0);
     int star_groups = 0;
-    const bool any_layout = (f & (MG_RAND_LAYOUT_MINOR | MG_RAND_LAYOUT_FULL)) != 0;
-    const bool minor = (f & MG_RAND_LAYOUT_MINOR) != 0;
+    const bool any_layout = LAYOUT == 0 ? false : (f & (MG_RAND_LAYOUT_MINOR | MG_RAND_LAYOUT_FULL)) != 0;
+    const bool minor = LAYOUT == 0 ? false : (f & MG_RAND_LAYOUT_MINOR) != 0;
     int ents[16]; bool rr[16]; double rl[16]; int n = 0;
-    if (cfg.task == MG_TASK_MOVE_TO_REGION) {
+    if (task_is<TASK>(cfg.task, MG_TASK_MOVE_TO_REGION)) {
         double gx = -0.62, gy = -0.17, gh = 0.76, gw = 0.75;
         if (any_layout) randomise_hw(S, e, gh, gw, minor ? JITTER_TARGET_BOUND : -1.0, gh, gw);
         int colour = MG_COL_BLUE;
@@ -457,7 +462,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
             randomise_all(S, L, e, lane, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl);
         }
-    } else if (cfg.task == MG_TASK_MOVE_TO_CORNER) {
+    } else if (task_is<TASK>(cfg.task, MG_TASK_MOVE_TO_CORNER)) {
         double rx = mt_double(S, e), ry = mt_double(S, e);
         inst_robot(S, L, e, B, rx, ry, 0.55 * 3.141592653589793);
         int colour = MG_COL_RED, type = MG_SHAPE_SQUARE;
@@ -469,8 +474,8 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
             randomise_all(S, L, e, lane, ents, n, rr, JITTER_POS_BOUND, rl);
         }
-    } else if (cfg.task == MG_TASK_CLUSTER_COLOUR || cfg.task == MG_TASK_CLUSTER_SHAPE) {
-        int by = cfg.task == MG_TASK_CLUSTER_SHAPE ? 1 : 0;
+    } else if (task_is<TASK>(cfg.task, MG_TASK_CLUSTER_COLOUR) || task_is<TASK>(cfg.task, MG_TASK_CLUSTER_SHAPE)) {
+        int by = task_is<TASK>(cfg.task, MG_TASK_CLUSTER_SHAPE) ? 1 : 0;
         int nblk = 8;
         bool count = (f & MG_RAND_SHAPE_COUNT) != 0;
         if (count) nblk = mt_randint(S, e, 7, 10 + 1);
@@ -491,7 +496,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
         }
         inst_robot(S, L, e, B, CC_ROBOT[by][0], CC_ROBOT[by][1], CC_ROBOT[by][2]);
         if (any_layout) {
-            bool full = (f & MG_RAND_LAYOUT_FULL) != 0;
+            bool full = LAYOUT == 0 ? false : (f & MG_RAND_LAYOUT_FULL) != 0;
             ents[0] = 1 + nblk;
             for (int i = 0; i < nblk; i++) ents[1 + i] = 1 + i;
             n = nblk + 1;
@@ -499,7 +504,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
             randomise_all(S, L, e, lane, ents, n, rr, full ? -1.0 : JITTER_POS_BOUND, rl);
         }
-    } else if (cfg.task == MG_TASK_MAKE_LINE) { // make_line.py:86-132
+    } else if (task_is<TASK>(cfg.task, MG_TASK_MAKE_LINE)) { // make_line.py:86-132
         int nblk = 4;
         const bool count = (f & MG_RAND_SHAPE_COUNT) != 0;
         if (count) nblk = mt_randint(S, e, 3, 4 + 1);
@@ -520,7 +525,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             S.nbodies[e] = B.nb; S.nshapes[e] = B.ns; S.ncons[e] = B.nc;
             randomise_all(S, L, e, lane, ents, n, rr, minor ? JITTER_POS_BOUND : -1.0, rl);
         }
-    } else if (cfg.task == MG_TASK_FIND_DUPE) { // find_dupe.py:62-199
+    } else if (task_is<TASK>(cfg.task, MG_TASK_FIND_DUPE)) { // find_dupe.py:62-199
         int qcol = MG_COL_YELLOW, qtype = MG_SHAPE_PENTAGON, cols[6], types[6];
         for (int i = 0; i < 6; i++) { cols[i] = FD_OUT_COLOURS[i]; types[i] = FD_OUT_TYPES[i]; }
         const bool count = (f & MG_RAND_SHAPE_COUNT) != 0;
@@ -562,7 +567,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
                     S.overflow[e] |= 2 | 64;
             }
         }
-    } else if (cfg.task == MG_TASK_FIX_COLOUR) { // fix_colour.py:67-176
+    } else if (task_is<TASK>(cfg.task, MG_TASK_FIX_COLOUR)) { // fix_colour.py:67-176
         const bool count = (f & MG_RAND_SHAPE_COUNT) != 0;
         const int nr = count ? mt_randint(S, e, 2, 3 + 1) : 3;
         int rcols[3], bcols[3], types[3];
@@ -618,7 +623,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
                 }
             }
         }
-    } else if (cfg.task == MG_TASK_PICK_AND_PLACE) { // pick_and_place.py:30-85
+    } else if (task_is<TASK>(cfg.task, MG_TASK_PICK_AND_PLACE)) { // pick_and_place.py:30-85
         inst_robot(S, L, e, B, 0.0, 0.0, 0.55 * 3.141592653589793); // entity 1: added before the shapes
         int cols[3], types[3];
         for (int i = 0; i < 3; i++) { // per shape: colour draw, then type draw
@@ -676,7 +681,7 @@ MG_DEV void reset_env(const MGState &S, const mg_library *L, int e, TaskCfg cfg)
             ttypes[0] = dtt[0]; ttypes[1] = dtt[1];
             for (int c = 0; c < 3; c++) { dtypes[c][0] = ddt[c][0]; dtypes[c][1] = ddt[c][1]; }
         }
-        bool full = (f & MG_RAND_LAYOUT_FULL) != 0;
+        bool full = LAYOUT == 0 ? false : (f & MG_RAND_LAYOUT_FULL) != 0;
         int first = S.nents[e];
         for (int i = 0; i < tcount; i++)
             inst_block(S, L, e, B, ttypes[i], target, 1, full ? 0.0 : dtp[i][0], full ? 0.0 : dtp[i][1], full ? 0.0 : dtp[i][2],
