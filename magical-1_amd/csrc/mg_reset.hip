@@ -2,6 +2,7 @@
 // the reset is off the step path (next-layout shadow): one out-of-line collide()
 // for its shape queries keeps this unit's compile time bounded (about 1 min instead of 35+)
 #define MG_COLLIDE_ATTR __device__ __attribute__((noinline))
+#include <cstdlib>
 #include "mg_launch.h"
 #include "mg_reset.h"
 __global__ void __launch_bounds__(64) seed_kernel(MGState S, const uint32_t *__restrict__ seeds) {
@@ -15,10 +16,12 @@ __global__ void __launch_bounds__(64) seed_kernel(MGState S, const uint32_t *__r
 template <int TASK, int LAYOUT>
 __global__ void __launch_bounds__(64) reset_kernel(MGState S, const mg_library *__restrict__ L, TaskCfg cfg,
                                                         const uint8_t *__restrict__ mask) {
-    const int e = blockIdx.x;
-    if (e >= S.n_envs || (mask && !mask[e])) return;
     cfg.coop = 1;
-    reset_env<TASK, LAYOUT>(S, L, e, cfg);
+    // grid-stride over the envs (a masked launch may run fewer wavefronts than envs: mg_launch_reset)
+    for (int e = blockIdx.x; e < S.n_envs; e += gridDim.x) {
+        if (mask && !mask[e]) continue;
+        reset_env<TASK, LAYOUT>(S, L, e, cfg);
+    }
 }
 
 static int grid64(const MGState &S) { return (S.n_envs + 63) / 64; }
@@ -38,7 +41,11 @@ hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, c
     auto k = reset_kernel<-1, -1>;
     if (!layout && cfg.task == MG_TASK_MOVE_TO_REGION) k = reset_kernel<MG_TASK_MOVE_TO_REGION, 0>;
     else if (!layout && cfg.task == MG_TASK_MOVE_TO_CORNER) k = reset_kernel<MG_TASK_MOVE_TO_CORNER, 0>;
-    hipLaunchKernelGGL(k, dim3(S.n_envs), dim3(64), 0, st, S, L, cfg, mask);
+    // masked robot-scene resets (the auto-reset: ~1 / episode length of the envs per step): a capped grid
+    // whose wavefronts scan the mask (MG_RESET_WAVES, A/B; 0 = one wavefront per env)
+    static const int cap = getenv("MG_RESET_WAVES") ? atoi(getenv("MG_RESET_WAVES")) : 0;
+    const int grid = (mask && cap > 0 && k != reset_kernel<-1, -1> && S.n_envs > cap) ? cap : S.n_envs;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(64), 0, st, S, L, cfg, mask);
     return hipGetLastError();
 }
 
