@@ -27,7 +27,10 @@ struct RenderOut {
 };
 
 hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream_t st);
-hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, const uint8_t *mask, hipStream_t st);
+// max_waves > 0 (masked launches only): at most that many wavefronts, each resetting the masked envs of its
+// grid-stride range in turn; 0: one wavefront per env
+hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, const uint8_t *mask, hipStream_t st,
+                           int max_waves = 0);
 // LDS-resident substeps: per-env slot caps of a task and envs per workgroup
 struct StepCaps { int nb, ns, nc, na, blk, shw; };  // shw: world-space shape scratch per lane in LDS
 size_t mg_step_lds_bytes(const StepCaps &c, int blk);

@@ -36,15 +36,13 @@ hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream
 // is a launch over every env that mostly exits at once, and with the generic kernel's register file (every
 // task's samplers, the rejection sampler's collide) each of those wavefronts waited for a whole SIMD to drain
 // when the render of another env chunk was running (0.03 ms alone, 0.17 ms beside it).
-hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, const uint8_t *mask, hipStream_t st) {
+hipError_t mg_launch_reset(const MGState &S, const mg_library *L, TaskCfg cfg, const uint8_t *mask, hipStream_t st,
+                           int max_waves) {
     const bool layout = (cfg.flags & (MG_RAND_LAYOUT_MINOR | MG_RAND_LAYOUT_FULL)) != 0;
     auto k = reset_kernel<-1, -1>;
     if (!layout && cfg.task == MG_TASK_MOVE_TO_REGION) k = reset_kernel<MG_TASK_MOVE_TO_REGION, 0>;
     else if (!layout && cfg.task == MG_TASK_MOVE_TO_CORNER) k = reset_kernel<MG_TASK_MOVE_TO_CORNER, 0>;
-    // masked robot-scene resets (the auto-reset: ~1 / episode length of the envs per step): a capped grid
-    // whose wavefronts scan the mask (MG_RESET_WAVES, A/B; 0 = one wavefront per env)
-    static const int cap = getenv("MG_RESET_WAVES") ? atoi(getenv("MG_RESET_WAVES")) : 0;
-    const int grid = (mask && cap > 0 && k != reset_kernel<-1, -1> && S.n_envs > cap) ? cap : S.n_envs;
+    const int grid = (mask && max_waves > 0 && S.n_envs > max_waves) ? max_waves : S.n_envs;
     hipLaunchKernelGGL(k, dim3(grid), dim3(64), 0, st, S, L, cfg, mask);
     return hipGetLastError();
 }

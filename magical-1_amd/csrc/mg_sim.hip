@@ -46,6 +46,8 @@ struct mg_sim {
     hipEvent_t ev_copied, ev_prepared;
     int shadow_ok;         // every env's shadow holds its next layout (set by a full mg_reset)
     int shadow_pending;    // a reset_kernel on SH is in flight on the side stream
+    int reset_waves;          // auto-reset launches: wavefronts cap (0: one per env; MG_RESET_WAVES, A/B)
+    int reset_waves_shadow;   // the shadow's next-layout launches: the same (MG_RESET_WAVES_SHADOW)
     int force_render_retry;   // tests: the first k render classes of the chain hand every (env, view) on
     int scache_mode;          // tests: RenderOut::scache_mode
     mg_library *dlib;
@@ -313,7 +315,7 @@ static int shadow_handover(mg_sim *s, hipStream_t st, const uint8_t *mask, int t
     HIPC(hipEventRecord(s->ev_copied, st));
     HIPC(hipStreamWaitEvent(s->side, s->ev_copied, 0));
     TaskCfg cfg = {s->task, s->flags};
-    HIPC(mg_launch_reset(s->SH, s->dlib, cfg, s->pend, s->side));
+    HIPC(mg_launch_reset(s->SH, s->dlib, cfg, s->pend, s->side, s->reset_waves_shadow));
     HIPC(hipEventRecord(s->ev_prepared, s->side));
     s->shadow_pending = 1;
     return 0;
@@ -357,6 +359,8 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     s->S.max_tries = 10000; // geom.py:198
     s->S.shw = nullptr;     // HBM-state kernels keep their narrowphase shapes in registers / scratch
     if (const char *mt = getenv("MG_DEBUG_MAX_TRIES")) s->S.max_tries = atoi(mt) > 0 ? atoi(mt) : 10000; // tests only
+    s->reset_waves = getenv("MG_RESET_WAVES") ? atoi(getenv("MG_RESET_WAVES")) : 0;
+    s->reset_waves_shadow = getenv("MG_RESET_WAVES_SHADOW") ? atoi(getenv("MG_RESET_WAVES_SHADOW")) : 0;
     if (const char *rr = getenv("MG_DEBUG_RENDER_RETRY")) s->force_render_retry = atoi(rr);                 // tests only
     else s->force_render_retry = 0;
     s->scache_mode = getenv("MG_DEBUG_SCACHE") ? atoi(getenv("MG_DEBUG_SCACHE")) : 0;                    // tests only
@@ -479,7 +483,7 @@ int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
             const int rc = shadow_handover(s, st, s->reset_mask, 1);
             if (rc) return rc;
         } else {
-            HIPC(mg_launch_reset(s->S, s->dlib, cfg, s->reset_mask, st));
+            HIPC(mg_launch_reset(s->S, s->dlib, cfg, s->reset_mask, st, s->reset_waves));
         }
     }
     if (ev) HIPC(hipEventRecord(ev[2], st));
