@@ -20,7 +20,6 @@ so the caller may overwrite its action tensor right after `step()` returns.
 """
 import collections
 import ctypes
-import os
 
 import torch
 
@@ -66,10 +65,8 @@ class PipelinedVecEnv:
             for k, v in s0.output_buffers().items() if k != "target")
         for k, sim in enumerate(self.sims):
             sim.bind_outputs({key: buf[b[k]:b[k + 1]] for key, buf in self.buffers.items()})
-        # MAGICAL_AMD_POOL_PRIO="p0,p1,...": per-chunk stream priorities (A/B; default all normal)
-        prio = [int(x) for x in os.environ.get("MAGICAL_AMD_POOL_PRIO", "").split(",") if x.strip()]
-        self.streams = [torch.cuda.Stream(self.device, priority=prio[k] if k < len(prio) else 0)
-                        for k in range(chunks)]
+        # (a high-priority stream for chunk 0 measured no different, round 4: profiles/r04_resetwaves/)
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(chunks)]
         self.abuf = torch.zeros((2, num_envs), dtype=torch.uint8, device=self.device)
         # done[k][slot]: chunk k finished the step that read action slot `slot`
         self.done_ev = [[None, None] for _ in range(chunks)]

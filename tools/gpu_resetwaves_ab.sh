@@ -15,7 +15,6 @@ for env in MoveToRegion-Demo-LoRes4E-v0 MoveToCorner-Demo-LoRes4E-v0; do
     python3 -c "import json; d=json.loads(open('$log').read().strip().splitlines()[-1]); print('$env waves $w', round(d['value']), d['ms_per_step'], d['kernel_ms_per_step'])"
   done
 done
-bash tools/gpu_poolprio_ab.sh pp
 MG_RESET_WAVES_SHADOW=16 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "(rollout_parity or reset_paths or layout_retry) and (Cluster or MatchRegions or FindDupe)" \
     --timeout 120 --timeout-method thread > "$OUT/pytest_shadow.log" 2>&1 || { echo "pytest shadow FAIL"; tail -30 "$OUT/pytest_shadow.log"; exit 1; }
 tail -1 "$OUT/pytest_shadow.log"
