@@ -685,53 +685,6 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     }
     RG_SYNC();
     MG_PROF(13);
-    uint8_t *ring = view == 0 ? S.hist_allo : S.hist_ego;
-    const size_t FR = (size_t)MG_LORES * MG_LORES * 3;
-    const bool fresh = S.episode_steps[e] == 0;
-    const int head = S.hist_head[view * S.N + e];
-    const int nh = fresh ? 0 : ((head + 1) & 3);
-    const int pp = out.preproc;
-    // frames-only outputs (compact multi-GPU gather): the current frame of each view, no stacks, no ring
-    // (the receivers rebuild the stacks: mg_restack)
-    const bool fo = out.frames_only != 0;
-    const bool stacked = !fo && (pp == MG_PREPROC_LORESSTACK || (pp == MG_PREPROC_LORES4E && view == 1) ||
-                                 (pp == MG_PREPROC_LORES4A && view == 0));
-    const bool plain = fo || pp != MG_PREPROC_LORESSTACK;   // the view's own current-frame output
-    // frame ring kept only where a stack reads it (LoRes3EA: ego ring, read by compose3ea_kernel)
-    const bool keep_ring = stacked || (!fo && pp == MG_PREPROC_LORES3EA && view == 1);
-    // Allocentric static layer.  The body-less entities (arena, goals) and the allo view matrix are fixed
-    // for the whole episode, so the episode's first allo frame also resolves every block with those
-    // entities alone (entity-bit classes: the outline layer tells the entities apart) and writes that frame
-    // to S.scache; every later allo frame copies it into each 4x4 block that no geom of a body can reach
-    // (its vertex bounds + RG_DMARGIN) and resolves only the others -- bands that no body reaches skip the
-    // fill edges, outline lines and resolve altogether.  A block outside every body geom's reach has the
-    // same pixels in the full scene as in the static-only scene, so the frame is bit-identical.
-    // (allo frames whose only output is the plain current frame: LoRes4E, LoRes3EA, frames-only; a stacked
-    // allo view writes ring and stack rows in every band anyway, and measured slower with the layer)
-    // The many-block tasks' classes are compiled without it: their scenes' blocks reach most bands, and
-    // the layer's code measured slower there (ClusterColour 2.72 -> 3.00 ms, MatchRegions 3.37 -> 3.41 ms).
-    constexpr bool kLayer = RG_SCACHE && SM::RG_MAXG <= 32;
-    const bool cview = kLayer && mode == 0 && view == 0 && out.scache_mode != 1 && !keep_ring && !stacked && plain;
-    const bool mk_cache = cview && fresh && !SM::ORDMAX;
-    const bool use_cache = cview && !fresh && S.scache_ok[e] != 0;
-    uint8_t *const scache = S.scache + (size_t)e * FR;
-    auto body_rows = [&](int &b0, int &b1) {   // wave 2: the bands a body geom can reach
-        int y0 = MG_RES, y1 = -1;
-        for (int g = lane; g < G; g += 64) {
-            if ((sm.smask >> sm.g_ent[g]) & 1u) continue;
-            const uint2 gi = sm.ginfo[g];
-            const int ymin = (int16_t)(gi.x & 0xFFFF) - RG_DMARGIN, ymax = (int16_t)(gi.x >> 16) + RG_DMARGIN;
-            y0 = ymin < y0 ? ymin : y0; y1 = ymax > y1 ? ymax : y1;
-        }
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int a = __shfl_xor(y0, off), b = __shfl_xor(y1, off);
-            y0 = a < y0 ? a : y0; y1 = b > y1 ? b : y1;
-        }
-        y0 = y0 > 0 ? y0 : 0; y1 = y1 < MG_RES - 1 ? y1 : MG_RES - 1;
-        b0 = y0 <= y1 ? y0 / RG_BAND : 0;
-        b1 = y0 <= y1 ? y1 / RG_BAND + 1 : 0;
-    };
     // ---- 4. per-geom bounds (vertex-parallel atomics) and the convexity premise of the fill: going
     //         round a polygon the sign of dy changes exactly twice (both vertex chains y-monotone) ----
     for (int g = tid; g < G; g += RG_THREADS) {
@@ -773,19 +726,6 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         sm.ginfo[g] = make_uint2((uint32_t)(uint16_t)ymin | ((uint32_t)(uint16_t)ymax << 16),
                                  (uint32_t)(uint16_t)xmin | ((uint32_t)(uint16_t)xmax << 16));
     }
-    // static-layer frames: the bands a body geom can reach are known from the bounds, so the outline items
-    // and fill edges are binned into those bands only (the others are copied from the layer, never drawn)
-    int cb0 = 0, cb1 = RG_NBANDS;
-    if (use_cache) {   // uniform over the workgroup
-        RG_SYNC();     // ginfo
-        if (tid >= 128) {
-            int b0, b1;
-            body_rows(b0, b1);
-            if (lane == 0) { sm.brng[0] = b0; sm.brng[1] = b1; }
-        }
-        RG_SYNC();
-        cb0 = sm.brng[0]; cb1 = sm.brng[1];
-    }
     if (sm.ndash > SM::RG_MAXDASH) sm.err = 1;
     if (sm.nsedge > SM::RG_MAXSEDGE) sm.err = 5;
     const int nitems = sm.nsedge + (sm.ndash < SM::RG_MAXDASH ? sm.ndash : SM::RG_MAXDASH);
@@ -801,8 +741,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
             if (xl >= 0 && xh + 1 <= MG_RES - 1 && ylo >= 0 && yhi <= MG_RES - 1) sm.sedge[i] |= 0x8000u;
         }
         ylo = ylo > 0 ? ylo : 0; yhi = yhi < MG_RES - 1 ? yhi : MG_RES - 1;
-        const int ba = ylo / RG_BAND > cb0 ? ylo / RG_BAND : cb0, bz = yhi / RG_BAND < cb1 - 1 ? yhi / RG_BAND : cb1 - 1;
-        for (int b = ba; b <= bz && ylo <= yhi; b++) atomicAdd(&sm.u.pre.bin_cnt[b], 1);
+        for (int b = ylo / RG_BAND; b <= yhi / RG_BAND && ylo <= yhi; b++) atomicAdd(&sm.u.pre.bin_cnt[b], 1);
     }
     for (int i = tid; i < SM::RG_MAXG * RG_BAND; i += RG_THREADS)
         (&sm.bspan[0][0])[i] = (uint32_t)RG_EMPTY | ((uint32_t)RG_EMPTY << 16);
@@ -813,8 +752,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         int xa, ya, xb, yb, side, r0, r1;
         bool lastrow;
         fill_edge(sm, ve, xa, ya, xb, yb, side, r0, r1, lastrow);
-        const int ba = r0 / RG_BAND > cb0 ? r0 / RG_BAND : cb0, bz = r1 / RG_BAND < cb1 - 1 ? r1 / RG_BAND : cb1 - 1;
-        for (int b = ba; b <= bz && r0 <= r1; b++) atomicAdd(&sm.u.pre.ebin_cnt[b], 1);
+        for (int b = r0 / RG_BAND; b <= r1 / RG_BAND && r0 <= r1; b++) atomicAdd(&sm.u.pre.ebin_cnt[b], 1);
     }
     RG_SYNC();
     if (tid < 64) {
@@ -847,8 +785,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         int ylo, yhi;
         item_rows(sm, i, ylo, yhi);
         ylo = ylo > 0 ? ylo : 0; yhi = yhi < MG_RES - 1 ? yhi : MG_RES - 1;
-        const int ba = ylo / RG_BAND > cb0 ? ylo / RG_BAND : cb0, bz = yhi / RG_BAND < cb1 - 1 ? yhi / RG_BAND : cb1 - 1;
-        for (int b = ba; b <= bz && ylo <= yhi; b++)
+        for (int b = ylo / RG_BAND; b <= yhi / RG_BAND && ylo <= yhi; b++)
             sm.bin[atomicAdd(&sm.u.pre.bin_cnt[b], 1)] = (uint16_t)i;
     }
     for (int v = tid; v < NV; v += RG_THREADS) {
@@ -856,8 +793,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         int xa, ya, xb, yb, side, r0, r1;
         bool lastrow;
         fill_edge(sm, ve, xa, ya, xb, yb, side, r0, r1, lastrow);
-        const int ba = r0 / RG_BAND > cb0 ? r0 / RG_BAND : cb0, bz = r1 / RG_BAND < cb1 - 1 ? r1 / RG_BAND : cb1 - 1;
-        for (int b = ba; b <= bz && r0 <= r1; b++)
+        for (int b = r0 / RG_BAND; b <= r1 / RG_BAND && r0 <= r1; b++)
             sm.bin[atomicAdd(&sm.u.pre.ebin_cnt[b], 1)] = (uint16_t)(ve | (lastrow ? 0x8000 : 0));
     }
     const int nsedge = sm.nsedge;
@@ -866,6 +802,36 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     if (out.debug_skip & 16) return;  // setup only
 #endif
     // ---- 5. bands ----
+    uint8_t *ring = view == 0 ? S.hist_allo : S.hist_ego;
+    const size_t FR = (size_t)MG_LORES * MG_LORES * 3;
+    const bool fresh = S.episode_steps[e] == 0;
+    const int head = S.hist_head[view * S.N + e];
+    const int nh = fresh ? 0 : ((head + 1) & 3);
+    const int pp = out.preproc;
+    // frames-only outputs (compact multi-GPU gather): the current frame of each view, no stacks, no ring
+    // (the receivers rebuild the stacks: mg_restack)
+    const bool fo = out.frames_only != 0;
+    const bool stacked = !fo && (pp == MG_PREPROC_LORESSTACK || (pp == MG_PREPROC_LORES4E && view == 1) ||
+                                 (pp == MG_PREPROC_LORES4A && view == 0));
+    const bool plain = fo || pp != MG_PREPROC_LORESSTACK;   // the view's own current-frame output
+    // frame ring kept only where a stack reads it (LoRes3EA: ego ring, read by compose3ea_kernel)
+    const bool keep_ring = stacked || (!fo && pp == MG_PREPROC_LORES3EA && view == 1);
+    // Allocentric static layer.  The body-less entities (arena, goals) and the allo view matrix are fixed
+    // for the whole episode, so the episode's first allo frame also resolves every block with those
+    // entities alone (entity-bit classes: the outline layer tells the entities apart) and writes that frame
+    // to S.scache; every later allo frame copies it into each 4x4 block that no geom of a body can reach
+    // (its vertex bounds + RG_DMARGIN) and resolves only the others -- bands that no body reaches skip the
+    // fill edges, outline lines and resolve altogether.  A block outside every body geom's reach has the
+    // same pixels in the full scene as in the static-only scene, so the frame is bit-identical.
+    // (allo frames whose only output is the plain current frame: LoRes4E, LoRes3EA, frames-only; a stacked
+    // allo view writes ring and stack rows in every band anyway, and measured slower with the layer)
+    // The many-block tasks' classes are compiled without it: their scenes' blocks reach most bands, and
+    // the layer's code measured slower there (ClusterColour 2.72 -> 3.00 ms, MatchRegions 3.37 -> 3.41 ms).
+    constexpr bool kLayer = RG_SCACHE && SM::RG_MAXG <= 32;
+    const bool cview = kLayer && mode == 0 && view == 0 && out.scache_mode != 1 && !keep_ring && !stacked && plain;
+    const bool mk_cache = cview && fresh && !SM::ORDMAX;
+    const bool use_cache = cview && !fresh && S.scache_ok[e] != 0;
+    uint8_t *const scache = S.scache + (size_t)e * FR;
     uint4 cpf = make_uint4(0, 0, 0, 0);   // wave 2, lanes 0-35: the next band's static-layer rows
     uint8_t *o_plain = view == 0 ? out.obs_allo : out.obs_ego;
     uint8_t *o_stack = pp == MG_PREPROC_LORESSTACK ? o_plain : out.obs_past;
@@ -931,6 +897,23 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     // bands outside the rows a body geom can reach are the static layer's rows, copied in bulk; the band
     // loop runs over [band0, band1) only.  Elsewhere (frame rings / stacks to write) it runs over every band.
     const bool brange = use_cache;
+    auto body_rows = [&](int &b0, int &b1) {   // wave 2: the bands a body geom can reach
+        int y0 = MG_RES, y1 = -1;
+        for (int g = lane; g < G; g += 64) {
+            if ((sm.smask >> sm.g_ent[g]) & 1u) continue;
+            const uint2 gi = sm.ginfo[g];
+            const int ymin = (int16_t)(gi.x & 0xFFFF) - RG_DMARGIN, ymax = (int16_t)(gi.x >> 16) + RG_DMARGIN;
+            y0 = ymin < y0 ? ymin : y0; y1 = ymax > y1 ? ymax : y1;
+        }
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int a = __shfl_xor(y0, off), b = __shfl_xor(y1, off);
+            y0 = a < y0 ? a : y0; y1 = b > y1 ? b : y1;
+        }
+        y0 = y0 > 0 ? y0 : 0; y1 = y1 < MG_RES - 1 ? y1 : MG_RES - 1;
+        b0 = y0 <= y1 ? y0 / RG_BAND : 0;
+        b1 = y0 <= y1 ? y1 / RG_BAND + 1 : 0;
+    };
     auto cache_prefetch = [&](int y0) {
         if (use_cache && tid >= 128 && tid < 128 + RG_BANDLO16)
             cpf = *(const uint4 *)(scache + (size_t)(y0 / 4) * RG_LOROW + 16 * (tid - 128));
@@ -944,7 +927,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     if (tid == 0) sm.nlong = 0;
     if (tid >= 128) {
         int b0 = 0, b1 = RG_NBANDS;
-        if (brange) { b0 = cb0; b1 = cb1; }   // found before the binning
+        if (brange) body_rows(b0, b1);
         if (lane == 0) { sm.brng[0] = b0; sm.brng[1] = b1; }
         if (b0 < b1) band_list(RG_BAND * b0);
         if (b0 < b1) cache_prefetch(RG_BAND * b0);
