@@ -49,10 +49,8 @@ bool mg_step_blk_ok(int variant, int blk) {
     return variant == 0 ? (blk == 1 || blk == 8 || blk == 64)
          : variant == 3 ? (blk == 1 || blk == 4)
          : variant == 4 ? blk == 1
-#ifdef MG_ALL_STEP_FORMS
-         : variant == 5 ? (blk == 16 || blk == 8)     // 8: comparison builds (pipelined chunks, round 4)
-#endif
-         : variant == 5 || variant == 6 ? blk == 16   // 8 / 4 envs per workgroup measured slower (round 4)
+         : variant == 5 ? (blk == 16 || blk == 8)     // 8: grids below 16 envs per CU (mg_sim.hip pick_step_blk)
+         : variant == 6 ? blk == 16                   // 8 / 4 envs per workgroup measured slower (round 4)
          : (blk == 1 || blk == 4 || blk == 16);
 }
 
@@ -66,10 +64,9 @@ hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, in
     MG_STEP_CASE(1, 1) MG_STEP_CASE(1, 4) MG_STEP_CASE(1, 16)
     MG_STEP_CASE(2, 1) MG_STEP_CASE(2, 4) MG_STEP_CASE(2, 16)
     MG_STEP_CASE(3, 1) MG_STEP_CASE(3, 4)
-    MG_STEP_CASE(5, 8)
 #endif
     MG_STEP_CASE(4, 1)
-    MG_STEP_CASE(5, 16) MG_STEP_CASE(6, 16)
+    MG_STEP_CASE(5, 16) MG_STEP_CASE(5, 8) MG_STEP_CASE(6, 16)
     MG_STEP_CASE(0, 1) MG_STEP_CASE(0, 8) MG_STEP_CASE(0, 64)
 #undef MG_STEP_CASE
     return hipErrorInvalidValue;

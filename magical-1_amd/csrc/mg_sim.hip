@@ -273,8 +273,13 @@ static int pick_step_variant(const StepCaps &c, int n_envs, int task) {
     return v;
 }
 
-static int pick_step_blk(int variant) {
+// Robot-only scenes (variant 5) below 16 envs x CUs run 8 envs per workgroup: the grid then still reaches
+// every CU, and a workgroup takes half a CU's LDS, so render workgroups of another env chunk fit beside it
+// (the pipelined pool's 2048-env chunks: MoveToRegion 2.82 -> 2.84 M env-steps/s, profiles/r04_check7/).  At 4096 envs and more,
+// 16 (8 measured slower there: two workgroups per CU, 0.83 vs 0.61 ms).
+static int pick_step_blk(int variant, int n_envs, int cus) {
     int b = variant == 0 ? 64 : variant == 3 || variant == 4 ? 1 : 16;
+    if (variant == 5 && n_envs < 16 * cus) b = 8;
     const char *ov = getenv(variant == 0 ? "MG_STEP_BLK0" : "MG_STEP_BLK"); // experiments
     if (ov && mg_step_blk_ok(variant, atoi(ov))) b = atoi(ov);
     return b;
@@ -383,7 +388,9 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     HIPC(hipMemcpy(s->dlib, cfg->library, sizeof(mg_library), hipMemcpyHostToDevice));
     s->caps = step_caps(cfg->task, cfg->rand_flags, cfg->num_envs, *(const mg_library *)cfg->library);
     s->step_variant = pick_step_variant(s->caps, cfg->num_envs, cfg->task);
-    s->step_blk = pick_step_blk(s->step_variant);
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
+    s->step_blk = pick_step_blk(s->step_variant, cfg->num_envs, cus);
     err = hipMalloc((void **)&s->reset_mask, (size_t)s->S.N);
     if (err != hipSuccess) { (void)hipFree(s->pool); (void)hipFree(s->dlib); delete s; return set_err(-12, "mg_create: hipMalloc mask"); }
     HIPC(hipMemset(s->reset_mask, 0, (size_t)s->S.N));

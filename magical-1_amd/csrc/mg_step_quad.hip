@@ -4,7 +4,6 @@
 
 template hipError_t launch_step_var<5, 16>(const MGState &, const mg_library *, TaskCfg, int, int, const uint8_t *, float *, uint8_t *, double *, uint8_t *, hipStream_t);
 template hipError_t launch_step_var<6, 16>(const MGState &, const mg_library *, TaskCfg, int, int, const uint8_t *, float *, uint8_t *, double *, uint8_t *, hipStream_t);
-#ifdef MG_ALL_STEP_FORMS   // comparison builds: 8 envs per workgroup (half the LDS, pipelined chunks A/B)
+// 8 envs per workgroup (half the LDS): robot-only grids below 16 envs per CU (mg_sim.hip pick_step_blk)
 template hipError_t launch_step_var<5, 8>(const MGState &, const mg_library *, TaskCfg, int, int, const uint8_t *, float *, uint8_t *, double *, uint8_t *, hipStream_t);
-#endif
 MG_PROF_READER(mg_prof_read_step_quad)
