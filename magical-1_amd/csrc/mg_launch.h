@@ -4,7 +4,9 @@
 #include <hip/hip_runtime.h>
 #include "mg_state.h"
 
-struct TaskCfg { int task, flags, coop; };  // coop: one env per 64-lane wave (reset_kernel_coop)
+// coop: one env per 64-lane wave (reset_kernel_coop); fused_reset: the step kernel runs the auto-reset of its
+// done envs itself (robot scenes without layout randomisation, mg_step)
+struct TaskCfg { int task, flags, coop, fused_reset; };
 
 struct RenderOut {
     uint8_t *full;        // [N][2][384][384][3] (full-resolution mode) or null

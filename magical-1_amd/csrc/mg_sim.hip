@@ -47,6 +47,7 @@ struct mg_sim {
     int shadow_ok;         // every env's shadow holds its next layout (set by a full mg_reset)
     int shadow_pending;    // a reset_kernel on SH is in flight on the side stream
     int reset_waves;          // auto-reset launches: wavefronts cap (0: one per env; MG_RESET_WAVES, A/B)
+    int no_fused_reset;       // MG_FUSED_RESET=0: the robot scenes' auto-reset as its own launch (A/B, tests)
     int reset_waves_shadow;   // the shadow's next-layout launches: the same (MG_RESET_WAVES_SHADOW)
     int force_render_retry;   // tests: the first k render classes of the chain hand every (env, view) on
     int scache_mode;          // tests: RenderOut::scache_mode
@@ -365,6 +366,7 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     s->S.shw = nullptr;     // HBM-state kernels keep their narrowphase shapes in registers / scratch
     if (const char *mt = getenv("MG_DEBUG_MAX_TRIES")) s->S.max_tries = atoi(mt) > 0 ? atoi(mt) : 10000; // tests only
     s->reset_waves = getenv("MG_RESET_WAVES") ? atoi(getenv("MG_RESET_WAVES")) : 0;
+    s->no_fused_reset = getenv("MG_FUSED_RESET") && atoi(getenv("MG_FUSED_RESET")) == 0;
     // the shadow's next layouts run beside the step stream's kernels: 512 wavefronts scanning the pending mask
     // instead of one 352-VGPR wavefront per env, most of which only exit (ClusterColour 1.458 -> 1.468 M,
     // MatchRegions 1.329 -> 1.358 M env-steps/s, same box; the in-place robot-scene resets gained nothing)
@@ -482,6 +484,11 @@ int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
     HIPC(hipSetDevice(s->device));
     hipStream_t st = as_stream(stream);
     TaskCfg cfg = {s->task, s->flags};
+    // robot scenes without layout randomisation: the step kernel runs the auto-reset itself (mg_stepk.h)
+    const bool layout = (s->flags & (MG_RAND_LAYOUT_MINOR | MG_RAND_LAYOUT_FULL)) != 0;
+    cfg.fused_reset = s->auto_reset && !s->shadow_ok && !layout && !s->no_fused_reset &&
+                      ((s->task == MG_TASK_MOVE_TO_REGION && s->step_variant == 5) ||
+                       (s->task == MG_TASK_MOVE_TO_CORNER && s->step_variant == 6));
     hipEvent_t *ev = nullptr;
     if (s->timing && s->ev_used + 4 <= s->ev.size()) { ev = &s->ev[s->ev_used]; s->ev_used += 4; }
     if (ev) HIPC(hipEventRecord(ev[0], st));
@@ -492,7 +499,7 @@ int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
         if (s->shadow_ok) {
             const int rc = shadow_handover(s, st, s->reset_mask, 1);
             if (rc) return rc;
-        } else {
+        } else if (!cfg.fused_reset) {
             HIPC(mg_launch_reset(s->S, s->dlib, cfg, s->reset_mask, st, s->reset_waves));
         }
     }

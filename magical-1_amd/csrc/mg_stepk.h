@@ -8,6 +8,7 @@
 #include "mg_step.h"
 #include "mg_stepq.h"
 #include "mg_score.h"
+#include "mg_reset.h"
 
 // slot caps of every compiled form: the LDS variants of mg_launch.h, plus the QL-lanes-per-env forms of the
 // compile-time scenes (5: the caps of 1 with two world-shape slots per lane in LDS -- 2 x 64 per workgroup,
@@ -256,8 +257,17 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
     if (reward) reward[e] = (float)((cfg.flags & MG_DEBUG_REWARD) ? debug_reward(S, L, e, cfg.task) : sc);
     if (done) done[e] = d ? 1 : 0;
     if (eval_score) eval_score[e] = sc;
-    // VecEnv auto-reset (next obs = first frame of the new episode) runs as reset_kernel on this mask
-    if (reset_mask) reset_mask[e] = (d && auto_reset) ? 1 : 0;
+    // VecEnv auto-reset (next obs = first frame of the new episode) runs as reset_kernel on this mask -- or,
+    // for the robot scenes without layout randomisation, here: their reset is serial straight-line code (no
+    // rejection sampling), so the env's own lane runs it and the step saves a launch (cfg.fused_reset)
+    if constexpr (VAR == 5 || VAR == 6) {
+        if (cfg.fused_reset && d && auto_reset) {
+            TaskCfg rc = cfg;
+            rc.coop = 0;
+            reset_env<VAR == 5 ? MG_TASK_MOVE_TO_REGION : MG_TASK_MOVE_TO_CORNER, 0>(S, L, e, rc);
+        }
+    }
+    if (reset_mask) reset_mask[e] = (d && auto_reset && !cfg.fused_reset) ? 1 : 0;
     MG_PP(P, 7);
     MG_PP_END(P, (threadIdx.x & 63) == 0, 32);
 }

@@ -404,6 +404,10 @@ RESET_PATHS = [
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 40, 7, {"MG_RESET_PREFETCH": "0"}),
     ("ClusterColour-TestAll-LoResStack-v0", 66, 30, 4, {}),
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, 5, {"MG_RESET_PREFETCH": "1"}),
+    # the robot scenes' auto-reset: fused into the step kernel (default) and as its own launch
+    ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, 5, {}),
+    ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, 6, {}),
+    ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, 6, {"MG_FUSED_RESET": "0"}),
     ("PickAndPlace-Demo-LoResCHW4A-v0", 8, 30, 4, {}),
     ("FindDupe-TestAll-LoRes4E-v0", 66, 30, 1, {}),
 ]
