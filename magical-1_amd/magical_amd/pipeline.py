@@ -167,5 +167,7 @@ class PipelinedVecEnv:
         return out
 
     def close(self):
+        for st in self.streams:   # the chunks' queued kernels read the simulators' memory
+            st.synchronize()
         for sim in self.sims:
             sim.close()
