@@ -171,3 +171,9 @@ class PipelinedVecEnv:
             st.synchronize()
         for sim in self.sims:
             sim.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
