@@ -161,12 +161,14 @@ __device__ __forceinline__ void env_substeps_coop(const MGState &V, const mg_lib
     const double dt = L->dt;
     __syncthreads();
     const CoopPlan Q = coop_plan(V, lane);
+    // robot.update() before every space.step() (base_env.py:248-255), on lane 0 right after the previous
+    // substep's closing barrier: space_step_coop reads only its step scalars before its first barrier, and
+    // the robot update writes the control body and the finger springs' rates (as mg_stepq.h)
+    if (lane == 0) robot_update(V, L, 0);
     for (int i = 0; i < 10; i++) {
-        __syncthreads();
-        if (lane == 0) robot_update(V, L, 0);
-        __syncthreads();
         MG_PP(P, 0);
-        space_step_coop(V, L, dt, lane, Q, P);
+        space_step_coop(V, L, dt, lane, Q, P);   // ends with a workgroup barrier
+        if (lane == 0 && i < 9) robot_update(V, L, 0);
     }
 }
 

@@ -215,13 +215,20 @@ MG_DEV void space_step_quad(const MGState &S, const mg_library *L, int e, int su
 template <int NCS, int QL, bool LDS_SHAPES>
 __device__ __forceinline__ void env_substeps_quad(const MGState &V, const mg_library *L, int ev, int sub, int a,
                                                   MGProf &P) {
-    if (sub == 0) robot_set_action(V, L, ev, a < 18 ? a : 0);
+    // robot.update() before every space.step() (base_env.py:248-255).  From the second substep on it runs on
+    // sub-lane 0 right after that lane's solver sweep of the previous substep, in the same phase: it reads
+    // angles and rotation caches (the sweep changes velocities only) and writes the control body's velocity
+    // and the finger springs' rates, which the next phase's barrier publishes -- one barrier phase fewer per
+    // substep, the same operations in the same order.
+    if (sub == 0) {
+        robot_set_action(V, L, ev, a < 18 ? a : 0);
+        robot_update<true>(V, L, ev);
+    }
     const double dt = L->dt;
     for (int i = 0; i < 10; i++) {
-        __syncthreads();
-        if (sub == 0) robot_update<true>(V, L, ev);
         MG_PP(P, 0);
-        space_step_quad<NCS, QL, LDS_SHAPES>(V, L, ev, sub, dt, P);
+        space_step_quad<NCS, QL, LDS_SHAPES>(V, L, ev, sub, dt, P);   // starts with a workgroup barrier
+        if (sub == 0 && i < 9) robot_update<true>(V, L, ev);
     }
     __syncthreads();
 }
