@@ -64,8 +64,6 @@ hipError_t mg_launch_compose3ea(const MGState &S, const uint8_t *obs_allo, const
 // profiling builds (-DMG_PROFILE): copy and clear each translation unit's phase timers
 hipError_t mg_prof_read_physics(unsigned long long *out64);
 hipError_t mg_prof_read_reset(unsigned long long *out64);
-hipError_t mg_prof_read_step_robot(unsigned long long *out64);
-hipError_t mg_prof_read_step_v3(unsigned long long *out64);
 hipError_t mg_prof_read_step_v4(unsigned long long *out64);
 hipError_t mg_prof_read_step_hbm(unsigned long long *out64);
 hipError_t mg_prof_read_raster(unsigned long long *out64);

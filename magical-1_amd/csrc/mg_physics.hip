@@ -1,7 +1,8 @@
 // mg_physics.hip -- step-kernel dispatch: the compiled form for a scene's slot caps (5/6: compile-time
 // constraint lists with 4 lanes per env, 4: cooperative LDS view with runtime lists, one env per wavefront,
 // 0: HBM state for scenes beyond the LDS caps) and envs per workgroup.  The forms live in mg_step_*.hip (one
-// translation unit each); the superseded one-lane forms 1/2/3 only in comparison builds (MG_ALL_STEP_FORMS).
+// translation unit each).  The one-lane forms 1/2/3 that 5/6/4 superseded were deleted in round 5 (their A/B
+// results are in DESIGN.md); variants 1/2/3 survive only as the slot caps mg_step_variant matches.
 #include "mg_launch.h"
 #include "mg_phys.h"   // sizeof(ShapeW) of the LDS views
 
@@ -43,15 +44,11 @@ int mg_step_variant(const StepCaps &c, int n_envs) {
 
 // envs per workgroup: compiled sizes only
 bool mg_step_blk_ok(int variant, int blk) {
-#ifndef MG_ALL_STEP_FORMS
-    if (variant >= 1 && variant <= 3) return false;
-#endif
     return variant == 0 ? (blk == 1 || blk == 8 || blk == 64)
-         : variant == 3 ? (blk == 1 || blk == 4)
          : variant == 4 ? blk == 1
          : variant == 5 ? (blk == 16 || blk == 8)     // 8: grids below 16 envs per CU (mg_sim.hip pick_step_blk)
-         : variant == 6 ? blk == 16                   // 8 / 4 envs per workgroup measured slower (round 4)
-         : (blk == 1 || blk == 4 || blk == 16);
+         : variant == 6 ? (blk == 16 || blk == 8 || blk == 4)   // 4: forms test only
+         : false;
 }
 
 hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, int variant, int blk, int max_steps,
@@ -60,13 +57,8 @@ hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, in
 #define MG_STEP_CASE(V, B) \
     if (variant == V && blk == B) \
         return launch_step_var<V, B>(S, L, cfg, max_steps, auto_reset, actions, reward, done, eval_score, reset_mask, st);
-#ifdef MG_ALL_STEP_FORMS   // comparison builds only (build.py --all-forms): the superseded one-lane forms
-    MG_STEP_CASE(1, 1) MG_STEP_CASE(1, 4) MG_STEP_CASE(1, 16)
-    MG_STEP_CASE(2, 1) MG_STEP_CASE(2, 4) MG_STEP_CASE(2, 16)
-    MG_STEP_CASE(3, 1) MG_STEP_CASE(3, 4)
-#endif
     MG_STEP_CASE(4, 1)
-    MG_STEP_CASE(5, 16) MG_STEP_CASE(5, 8) MG_STEP_CASE(6, 16)
+    MG_STEP_CASE(5, 16) MG_STEP_CASE(5, 8) MG_STEP_CASE(6, 16) MG_STEP_CASE(6, 8) MG_STEP_CASE(6, 4)
     MG_STEP_CASE(0, 1) MG_STEP_CASE(0, 8) MG_STEP_CASE(0, 64)
 #undef MG_STEP_CASE
     return hipErrorInvalidValue;
@@ -75,10 +67,6 @@ hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, in
 hipError_t mg_prof_read_physics(unsigned long long *out) {
     hipError_t e;
     if ((e = mg_prof_read_reset(out)) != hipSuccess) return e;
-#ifdef MG_ALL_STEP_FORMS
-    if ((e = mg_prof_read_step_robot(out)) != hipSuccess) return e;
-    if ((e = mg_prof_read_step_v3(out)) != hipSuccess) return e;
-#endif
     if ((e = mg_prof_read_step_v4(out)) != hipSuccess) return e;
     if ((e = mg_prof_read_step_quad(out)) != hipSuccess) return e;
     return mg_prof_read_step_hbm(out);

@@ -280,7 +280,7 @@ static int pick_step_variant(const StepCaps &c, int n_envs, int task) {
 // 16 (8 measured slower there: two workgroups per CU, 0.83 vs 0.61 ms).
 static int pick_step_blk(int variant, int n_envs, int cus) {
     int b = variant == 0 ? 64 : variant == 3 || variant == 4 ? 1 : 16;
-    if (variant == 5 && n_envs < 16 * cus) b = 8;
+    if ((variant == 5 || variant == 6) && n_envs < 16 * cus) b = 8;
     const char *ov = getenv(variant == 0 ? "MG_STEP_BLK0" : "MG_STEP_BLK"); // experiments
     if (ov && mg_step_blk_ok(variant, atoi(ov))) b = atoi(ov);
     return b;

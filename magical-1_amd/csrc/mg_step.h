@@ -217,31 +217,6 @@ __host__ __device__ constexpr ConsDesc static_cons(int c) {
                                 {MG_C_ROTLIMIT, 0, 5}, {MG_C_MOTOR, 0, 5},   {MG_C_PIVOT, -1, 6},  {MG_C_GEAR, -1, 6}};
     return T[c];
 }
-template <int NC, int C = 0>
-MG_DEV void static_prestep(const MGState &S, int e, double dt) {
-    if constexpr (C < NC) {
-        constexpr ConsDesc d = static_cons(C);
-        cons_prestep_impl(S, e, C, d.a, d.b, d.type, dt);
-        static_prestep<NC, C + 1>(S, e, dt);
-    }
-}
-template <int NC, int C = 0>
-MG_DEV void static_cached(const MGState &S, int e, double dt_coef) {
-    if constexpr (C < NC) {
-        constexpr ConsDesc d = static_cons(C);
-        cons_cached_impl(S, e, C, d.a, d.b, d.type, dt_coef);
-        static_cached<NC, C + 1>(S, e, dt_coef);
-    }
-}
-template <int NC, int C = 0>
-MG_DEV void static_apply(const MGState &S, int e, double dt) {
-    if constexpr (C < NC) {
-        constexpr ConsDesc d = static_cons(C);
-        cons_apply_impl(S, e, C, d.a, d.b, d.type, dt);
-        static_apply<NC, C + 1>(S, e, dt);
-    }
-}
-
 // ---- arbiters ------------------------------------------------------------
 // (ta, ba) / (tb, bb): world-shape type and body of the pair's shapes A / B in broadphase order
 MG_DEV void arbiter_update_t(const MGState &S, const mg_library *L, int e, int key, int ta, int ba, int tb, int bb,
@@ -676,8 +651,7 @@ MG_DEV void static_solve(const MGState &S, int e, double dt, double dt_coef, int
 }
 
 // ---- cpSpaceStep -----------------------------------------------------------
-// NCS > 0: the constraint list is the compile-time static_cons(0 .. NCS-1) (asserted by the caller)
-template <int NCS = 0>
+// one lane per env on the HBM state (variant 0, scenes beyond the LDS forms' caps): runtime constraint lists
 MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, MGProf &P) {
     uint32_t stamp = S.stamp[e] + 1;
     S.stamp[e] = stamp;
@@ -697,12 +671,7 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
     for (int k = 0; k < ns; k++) shape_update_bb(S, L, e, k);
     MG_PP(P, 1);
     // broadphase + narrowphase, canonical order
-    // narrowphase operands: in the LDS view's per-lane shape scratch for the compile-time scenes (LDS
-    // latency instead of per-lane scratch memory), locals elsewhere
-    ShapeW locA, locW, locB;
-    constexpr bool LDS_SHAPES = NCS > 0 && step_variant_caps(NCS == 10 ? 1 : 2).shw > 0;
-    ShapeW &A = LDS_SHAPES ? S.shw[3 * e] : locA, &W = LDS_SHAPES ? S.shw[3 * e + 1] : locW;
-    ShapeW &B = LDS_SHAPES ? S.shw[3 * e + 2] : locB;
+    ShapeW A, W, B;   // narrowphase operands (per-lane scratch)
 #ifdef MG_EXP_NO_NARROW     // timing experiments only (tools/build_unit_variant.sh): no collisions at all
     ns = 0;
 #endif
@@ -748,24 +717,16 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
     nact = S.nactive[e];
     int nc = S.ncons[e];
     for (int i = 0; i < nact; i++) arbiter_prestep(S, L, e, AT(S.active, i), dt);
-    if constexpr (NCS > 0) static_prestep<NCS>(S, e, dt);
-    else for (int c = 0; c < nc; c++) cons_prestep(S, e, c, dt);
+    for (int c = 0; c < nc; c++) cons_prestep(S, e, c, dt);
     MG_PP(P, 4);
     // velocity integration is the identity here (no gravity, damping 1, no forces)
     double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
-    if constexpr (NCS > 0) {
-        static_solve<NCS>(S, e, dt, dt_coef, nact, P);
-        MG_PP(P, 6);
-        return;
-    }
     for (int i = 0; i < nact; i++) arbiter_cached(S, e, AT(S.active, i), dt_coef);
-    if constexpr (NCS > 0) static_cached<NCS>(S, e, dt_coef);
-    else for (int c = 0; c < nc; c++) cons_cached(S, e, c, dt_coef);
+    for (int c = 0; c < nc; c++) cons_cached(S, e, c, dt_coef);
     MG_PP(P, 5);
     for (int it = 0; it < 10; it++) {
         for (int i = 0; i < nact; i++) arbiter_apply(S, e, AT(S.active, i));
-        if constexpr (NCS > 0) static_apply<NCS>(S, e, dt);
-        else for (int c = 0; c < nc; c++) cons_apply(S, e, c, dt);
+        for (int c = 0; c < nc; c++) cons_apply(S, e, c, dt);
     }
     MG_PP(P, 6);
 }

@@ -1,6 +1,6 @@
 // mg_stepk.h -- the step kernel template (action decode, 10 x [Robot.update + cpSpaceStep], episode
 // counter, score) and its launcher.  Each form is instantiated in its own translation unit
-// (mg_step_robot.hip, mg_step_v3.hip, mg_step_v4.hip, mg_step_hbm.hip) so they compile in parallel;
+// (mg_step_quad.hip: 5 / 6, mg_step_v4.hip: 4, mg_step_hbm.hip: 0) so they compile in parallel;
 // mg_physics.hip dispatches.
 #pragma once
 #include <cstdio>
@@ -143,15 +143,14 @@ __device__ __forceinline__ int xcd_block(int b, int g) {
     return x * q + (x < r ? x : r) + (b >> 3);
 }
 
-// Robot.set_action + 10 x (Robot.update, cpSpaceStep): base_env.py:248-276
-template <int NCS>
+// Robot.set_action + 10 x (Robot.update, cpSpaceStep): base_env.py:248-276 (one lane per env, HBM state)
 __device__ __forceinline__ void env_substeps(const MGState &V, const mg_library *L, int ev, int a, MGProf &P) {
     robot_set_action(V, L, ev, a < 18 ? a : 0);
     const double dt = L->dt;
     for (int i = 0; i < 10; i++) {
         robot_update(V, L, ev);
         MG_PP(P, 0);
-        space_step<NCS>(V, L, ev, dt, P);
+        space_step(V, L, ev, dt, P);
     }
 }
 
@@ -178,11 +177,12 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
                                                   uint8_t *done, double *eval_score, uint8_t *reset_mask) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr StepCaps C = step_form_caps(VAR, BLK);
+    static_assert(VAR == 0 || VAR == 4 || VAR == 5 || VAR == 6, "compiled forms: 0 (HBM state), 4 (cooperative), 5 / 6");
     constexpr bool LDS = VAR != 0;
     constexpr bool COOP = VAR == 4;            // one env per workgroup of 64 lanes
     constexpr bool QUAD = VAR == 5 || VAR == 6; // QL lanes per env, BLK envs in one 64-lane workgroup
     constexpr int QL = QUAD ? 64 / BLK : 1;
-    constexpr int NCS = VAR == 3 || VAR == 4 ? 0 : C.nc; // compile-time constraint list (0: the env's runtime list)
+    constexpr int NCS = VAR == 4 ? 0 : C.nc;   // compile-time constraint list (0: the env's runtime list)
     const int lane = COOP ? (int)threadIdx.x : QUAD ? (int)threadIdx.x / QL : BLK == 1 ? 0 : (int)threadIdx.x;
     const int sub = QUAD ? (int)threadIdx.x % QL : 0;
     int e = xcd_block(blockIdx.x, gridDim.x) * BLK + (COOP ? 0 : lane);
@@ -237,20 +237,16 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
             __threadfence_block();
             __syncthreads();
             if (!own || sub != 0) return;
-        } else if constexpr (COOP) {
+        } else {   // COOP
             xfer_state(S, V, C, 0, e, true, true, lane, 64);
             __syncthreads();
             env_substeps_coop(V, L, lane, a, P);
             xfer_state(S, V, C, 0, e, false, true, lane, 64);
             __syncthreads();
             if (lane != 0) return;
-        } else {
-            xfer_state(S, V, C, lane, e, true, NCS == 0);
-            env_substeps<NCS>(V, L, lane, a, P);
-            xfer_state(S, V, C, lane, e, false);
         }
     } else {
-        env_substeps<0>(S, L, e, a, P);
+        env_substeps(S, L, e, a, P);
     }
     int steps = S.episode_steps[e] + 1;
     S.episode_steps[e] = steps;

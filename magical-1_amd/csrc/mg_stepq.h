@@ -219,7 +219,10 @@ __device__ __forceinline__ void env_substeps_quad(const MGState &V, const mg_lib
     // sub-lane 0 right after that lane's solver sweep of the previous substep, in the same phase: it reads
     // angles and rotation caches (the sweep changes velocities only) and writes the control body's velocity
     // and the finger springs' rates, which the next phase's barrier publishes -- one barrier phase fewer per
-    // substep, the same operations in the same order.
+    // substep, the same operations in the same order.  The first update reads rows (angles, rotation caches)
+    // and writes rows (the finger motors' rates) that the env's sibling lanes loaded into LDS in xfer_state:
+    // one barrier orders them, once per env-step.
+    __syncthreads();
     if (sub == 0) {
         robot_set_action(V, L, ev, a < 18 ? a : 0);
         robot_update<true>(V, L, ev);

@@ -30,25 +30,16 @@ UNITS = {  # translation unit -> headers it depends on (one unit per kernel fami
     "mg_replay.hip": ["mg_common.h"],
 }
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-Wno-unused-result"]
-# comparison builds only (--all-forms -> libmagical_sim_allforms.so, MAGICAL_AMD_EXP_LIB=allforms): the one-lane
-# step forms 1 / 2 / 3 that forms 5 / 6 / 4 superseded (round 4: out of the default library)
-ALL_FORMS_UNITS = {"mg_step_robot.hip": _STEP, "mg_step_v3.hip": _STEP}
 
 
 def _mtime(p):
     return os.path.getmtime(p) if os.path.exists(p) else 0.0
 
 
-def build(force=False, verbose=False, profile=False, all_forms=False):
+def build(force=False, verbose=False, profile=False):
     out = PROF_OUT if profile else OUT
     tag = "prof" if profile else "opt"
     units = dict(UNITS)
-    extra = []
-    if all_forms:
-        out = os.path.join(HERE, "libmagical_sim_allforms.so")
-        tag = "allf"
-        units.update(ALL_FORMS_UNITS)
-        extra = ["-DMG_ALL_STEP_FORMS"]
     os.makedirs(OBJDIR, exist_ok=True)
     procs, objs = [], []
     for unit, headers in units.items():
@@ -57,7 +48,7 @@ def build(force=False, verbose=False, profile=False, all_forms=False):
         deps = [os.path.join(CSRC, unit), INCLUDE] + [os.path.join(CSRC, h) for h in headers]
         if not force and _mtime(obj) > max(_mtime(d) for d in deps):
             continue
-        cmd = ["hipcc"] + FLAGS + extra + (["-DMG_PROFILE"] if profile else []) + ["-c", os.path.join(CSRC, unit),
+        cmd = ["hipcc"] + FLAGS + (["-DMG_PROFILE"] if profile else []) + ["-c", os.path.join(CSRC, unit),
                                                                          "-o", obj + ".tmp"]
         if verbose:
             print(" ".join(cmd), flush=True)
@@ -76,5 +67,4 @@ def build(force=False, verbose=False, profile=False, all_forms=False):
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, profile="--profile" in sys.argv,
-                all_forms="--all-forms" in sys.argv))
+    print(build(force="--force" in sys.argv, verbose=True, profile="--profile" in sys.argv))

@@ -133,18 +133,21 @@ class VecMagicalEnv:
         buf.frames_only = 1 if self.frames_only else 0
         native.check(self.lib.mg_bind_outputs(self.handle, ctypes.byref(buf)))
 
-    def bind_outputs(self, views, frames_only=False):
+    def bind_outputs(self, views, frames_only=False, target=None):
         """Write the following steps' outputs into caller-owned device tensors (e.g. views into one packed
         buffer per step, magical_amd.dist.PackedLayout): keys as output_buffers().  frames_only: 'allo' /
         'ego' receive only the current [n, 96, 96, 3] frames for every LoRes preprocessor (no stacks;
         magical_amd.dist's compact gather restacks on the receivers) -- changing the mode needs a reset.
-        PickAndPlace's target stays in the env's own persistent buffer (the simulator writes it only at
-        reset); callers copy it where they need it."""
+        PickAndPlace's target (written only at reset) stays in the env's own persistent buffer (views["target"]
+        is ignored: a per-step packed buffer would hold a stale one), unless `target` names a persistent [n, 4]
+        f64 tensor to use instead -- bind it before the reset that fills it (magical_amd.pipeline)."""
         if self.spec.preproc is None:
             raise ValueError("bind_outputs: the unwrapped 384^2 view is rendered on demand, not bound")
         self.obs_allo, self.obs_ego = views["allo"], views["ego"]
         self.obs_past = None if frames_only else views.get("past_obs")
         self.reward, self.done, self.eval_score = views["reward"], views["done"], views["eval_score"]
+        if self.target is not None and target is not None:
+            self.target = target
         self.frames_only = bool(frames_only)
         self._bind()
 

@@ -59,12 +59,15 @@ class PipelinedVecEnv:
         self.action_space, self.observation_space = s0.action_space, s0.observation_space
         if self.spec.preproc is None:
             raise ValueError("PipelinedVecEnv: LoRes preprocessors only (the 384^2 view is rendered on demand)")
-        # the pool's full-batch outputs; chunk k writes rows [bounds[k], bounds[k + 1])
+        # the pool's full-batch outputs; chunk k writes rows [bounds[k], bounds[k + 1]) on its own stream
+        # (PickAndPlace's target included: the auto-reset rewrites it inside the chunk's step, so it is complete
+        # only after wait(), like the observations -- ADVICE r4)
         self.buffers = collections.OrderedDict(
-            (k, torch.empty((num_envs,) + tuple(v.shape[1:]), dtype=v.dtype, device=self.device))
-            for k, v in s0.output_buffers().items() if k != "target")
+            (k, torch.zeros((num_envs,) + tuple(v.shape[1:]), dtype=v.dtype, device=self.device))
+            for k, v in s0.output_buffers().items())
         for k, sim in enumerate(self.sims):
-            sim.bind_outputs({key: buf[b[k]:b[k + 1]] for key, buf in self.buffers.items()})
+            views = {key: buf[b[k]:b[k + 1]] for key, buf in self.buffers.items()}
+            sim.bind_outputs(views, target=views.get("target"))
         # (a high-priority stream for chunk 0 measured no different, round 4: profiles/r04_resetwaves/)
         self.streams = [torch.cuda.Stream(self.device) for _ in range(chunks)]
         self.abuf = torch.zeros((2, num_envs), dtype=torch.uint8, device=self.device)
@@ -124,8 +127,8 @@ class PipelinedVecEnv:
         out = collections.OrderedDict([("allo", self.buffers["allo"]), ("ego", self.buffers["ego"])])
         if self.sims[0]._chw:
             out = collections.OrderedDict((k, v.permute(0, 3, 1, 2)) for k, v in out.items())
-        if self.sims[0].target is not None:
-            t = torch.cat([s.target for s in self.sims]).to(torch.float32)
+        if "target" in self.buffers:
+            t = self.buffers["target"].to(torch.float32)
             out["target_type"], out["target_colour"], out["target_position"] = t[:, 0:1], t[:, 1:2], t[:, 2:4]
         if "past_obs" in self.buffers:
             p = self.buffers["past_obs"]

@@ -117,14 +117,17 @@ def test_rollout_parity(name, n, steps):
 # every compiled step-kernel (and render-class) form, forced through the experiment switches read at mg_create
 # (MG_STEP_VARIANT: 0 = HBM state (the default for scenes beyond the LDS caps), 5/6 = compile-time
 # constraint lists with 4 lanes per env (robot scenes), 4 = LDS with runtime lists, one env per 64-lane
-# wavefront (every other scene); MG_STEP_BLK / MG_STEP_BLK0: envs per workgroup.  The superseded one-lane
-# forms 1/2/3 are only in comparison builds, magical_amd.build --all-forms)
+# wavefront (every other scene); MG_STEP_BLK / MG_STEP_BLK0: envs per workgroup)
 KERNEL_FORMS = [
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "8"}),
     # 4 lanes per env (16 envs per 64-lane workgroup; 70 envs leave shadow lanes in the last one)
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5"}),   # 8 envs per workgroup (small grid)
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5", "MG_STEP_BLK": "16"}),
-    ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "6"}),
+    ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "6", "MG_STEP_BLK": "16"}),
+    # robot + block scenes at 8 / 4 envs per workgroup (8 / 16 lanes per env; 8 is the default below 16 envs
+    # per CU, the pipelined pool's 2048-env chunks): removed in round 4 after a GPU fault, restored in round 5
+    ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "6", "MG_STEP_BLK": "8"}),
+    ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "6", "MG_STEP_BLK": "4"}),
     ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "1"}),
     ("ClusterColour-Demo-LoResStack-v0", 66, 30, {"MG_STEP_VARIANT": "4"}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "4"}),
@@ -393,6 +396,60 @@ def test_full_size_sampled_parity(name, n, steps, L):
     assert resets == len(pick) * (steps // (L or spec.max_episode_steps))
     assert int(vec.errors().abs().sum().item()) == 0
     vec.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n,steps", [("MoveToRegion-Demo-LoRes4E-v0", 4096, 85),
+                                          ("MoveToCorner-Demo-LoRes4E-v0", 4096, 165)])
+def test_full_size_pipelined_parity(name, n, steps):
+    """The configuration bench.py times for C2 / C3: magical_amd.pipeline.PipelinedVecEnv
+    with 2 chunks of 2048 envs (the 8-envs-per-workgroup step forms 5 / 6 and the auto-reset fused into the
+    step kernel), episode phases spread over the envs the oracle does not follow (so every step mixes resetting
+    and running envs in a workgroup), against the oracle every step on a spread of envs of both chunks:
+    observations bit-exact, body state within POSE_TOL, done / eval_score equal, >= 2 episode boundaries."""
+    from magical_amd import pipeline
+    spec = registry.lookup(name)
+    L = spec.max_episode_steps
+    seeds = [1000 + i for i in range(n)]
+    pool = pipeline.PipelinedVecEnv(name, n, chunks=2, seeds=seeds)
+    assert [s.num_envs for s in pool.sims] == [n // 2, n // 2]
+    h = n // 2
+    pick = sorted({0, 1, 7, 8, 63, 64, h - 1, h, h + 1, h + 9, n - 9, n - 1})
+    orc = {i: po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, L, seed=seeds[i]) for i in pick}
+    obs = pool.reset()
+    pool.wait()
+    for i in pick:
+        ref = oracle_obs_split(spec, orc[i].reset())
+        for k in obs:
+            assert np.array_equal(obs[k][i].cpu().numpy(), ref[k]), f"reset env {i} {k}"
+    phase = np.array([0 if i in orc else (i * 7) % L for i in range(n)], dtype=np.int32)
+    pool.set_episode_steps(torch.from_numpy(phase))
+    acts = np.random.RandomState(9).randint(0, 18, (steps, n)).astype(np.uint8)
+    a_dev = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    resets = 0
+    for t in range(steps):
+        a_dev.copy_(torch.from_numpy(acts[t]))
+        obs, rew, done, info = pool.step(a_dev)
+        pool.wait()
+        got = {k: v[pick].cpu().numpy() for k, v in obs.items()}
+        got_done, got_score = done[pick].cpu().numpy(), info["eval_score"][pick].cpu().numpy()
+        bodies = torch.cat([s.bodies()[0] for s in pool.sims])[pick].cpu().numpy()
+        for j, i in enumerate(pick):
+            o, r, d, s = orc[i].step(int(acts[t, i]))
+            assert bool(got_done[j]) == d and got_score[j] == s, f"step {t} env {i}"
+            if d:
+                o = orc[i].reset()
+                resets += 1
+            else:
+                b = orc[i].bodies()
+                diff = np.abs(bodies[j, :len(b)] - b).max()
+                assert diff <= POSE_TOL, f"step {t} env {i} body state diff {diff}"
+            ref = oracle_obs_split(spec, o)
+            for k in got:
+                assert np.array_equal(got[k][j], ref[k]), f"step {t} env {i} obs {k}"
+    assert resets == len(pick) * (steps // L) and steps // L >= 2
+    assert int((pool.errors() != 0).sum()) == 0
+    pool.close()
 
 
 # Auto-reset paths (mg_sim.hip): the next-layout shadow (default for the many-block tasks: the next
@@ -877,6 +934,7 @@ def test_single_env_reset_after_placement_error(monkeypatch, name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,n,chunks,L", [("MoveToRegion-Demo-LoRes4E-v0", 256, 2, 40),
                                              ("MoveToCorner-Demo-LoRes4E-v0", 96, 3, 25),
+                                             ("PickAndPlace-Demo-LoResCHW4A-v0", 64, 2, 15),
                                              ("ClusterColour-Demo-LoResStack-v0", 64, 3, 20)])
 def test_pipelined_pool_matches_batch(name, n, chunks, L):
     """magical_amd.pipeline: C simulators on C streams (env i of the pool seeded as env i of the batch) give the
