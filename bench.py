@@ -73,11 +73,23 @@ def render_bytes(preproc, frames_only=False):
     return obs_bytes(preproc) + ring
 
 
-def restack_bytes(preproc):
-    """mg_restack per received env-step: current frame read, 3 ring frames read, 1 ring frame written and
-    the 4-frame stack written, per stacked view (LoRes3EA: + the allo frame read)."""
+def restack_bytes(preproc, window=True, K=8):
+    """Receiver-side restack per received env-step and stacked view.  Window ring (mg_restack_window, the
+    default except LoRes3EA): the current frame read, written once channel-planar plus, on 3 of every K steps,
+    once more (the slots that keep the 4-frame window contiguous): FR + (1 + 3 / K) FR.  Materialised stacks
+    (mg_restack): current frame read, 3 ring frames read, 1 ring frame written and the 4-frame stack written
+    (LoRes3EA: + the allo frame read)."""
     views = 2 if preproc == "LoResStack" else 1
+    if window and preproc != "LoRes3EA":
+        return int(round(views * (FR + (1 + 3 / K) * FR)))
     return views * (FR + 3 * FR + FR + 4 * FR) + (FR if preproc == "LoRes3EA" else 0)
+
+
+def step_fraction(preproc, envs, ms_per_step):
+    """roofline.step_frac: SURVEY 8(d) bytes of the env-steps one GPU completes per step over the measured
+    ms_per_step, against the 8 TB/s HBM peak -- (achieved GB/s, fraction)."""
+    ach = survey_bytes(preproc) * envs / (ms_per_step * 1e-3) / 1e9
+    return ach, ach / HBM_PEAK_GBS
 
 
 def cpu_share():
@@ -146,11 +158,14 @@ def cpu_baseline(name, workers, steps, affinity, quota):
                                 f"the job may use {workers} of them)"}
 
 
-def load_pmc(kernel, workload, envs):
+def load_pmc(kernel, workload, envs, envs_per_launch=None):
     """PMC record of `kernel` (HBM bytes per launch, VALU issue fraction) from the committed passes, newest
-    first: profiles/r02_final/<workload>.traffic.json (tools/gpu_table.sh at the round's final build), then
-    profiles/r02_table/, then profiles/pmc_traffic.json -- only when collected on this workload and env count."""
-    for path in (os.path.join(ROOT, "profiles", "r04_final", f"{workload}.traffic.json"),
+    first: profiles/r05_final/<workload>.traffic.json (tools/gpu_table.sh at the round's final build), then
+    the earlier rounds' -- only when collected on this workload, env count and envs per launch (records without
+    envs_per_launch were collected unchunked: envs per launch = envs)."""
+    epl = envs if envs_per_launch is None else envs_per_launch
+    for path in (os.path.join(ROOT, "profiles", "r05_final", f"{workload}.traffic.json"),
+                 os.path.join(ROOT, "profiles", "r04_final", f"{workload}.traffic.json"),
                  os.path.join(ROOT, "profiles", "r03_final", f"{workload}.traffic.json"),
                  os.path.join(ROOT, "profiles", "r02_final", f"{workload}.traffic.json"),
                  os.path.join(ROOT, "profiles", "r02_table", f"{workload}.traffic.json"),
@@ -159,7 +174,8 @@ def load_pmc(kernel, workload, envs):
             continue
         with open(path) as f:
             rec = json.load(f).get(kernel)
-        if rec and rec.get("workload") == workload and rec.get("envs") == envs:
+        if rec and rec.get("workload") == workload and rec.get("envs") == envs and \
+                abs(rec.get("envs_per_launch", rec.get("envs")) - epl) < 1e-6:
             return rec
     return None
 
@@ -238,8 +254,14 @@ def main():
                          "the restack stream, beside the next step (value stays this rank's env-steps/s x W)")
     ap.add_argument("--chunks", default="auto",
                     help="env chunks pipelined on their own HIP streams (magical_amd.pipeline): an int, or auto = "
-                         "2 for the robot scenes (MoveToRegion / MoveToCorner: measured faster), 1 otherwise and "
-                         "under the all-gather")
+                         "2 for the robot scenes (MoveToRegion / MoveToCorner: measured faster), 1 otherwise "
+                         "(also under the all-gather: the collective waits for every chunk's stream)")
+    ap.add_argument("--iso-steps", type=int, default=20,
+                    help="chunked runs: steps of chunk 0 alone after the timed region, for the roofline's isolated "
+                         "per-kernel times (0: none)")
+    ap.add_argument("--restack", default="window", choices=("window", "materialize"),
+                    help="frames-mode receivers: window ring views (mg_restack_window) or materialised stacks "
+                         "(mg_restack)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -292,16 +314,15 @@ def main():
     seeds = [1000 + rank * n + i for i in range(n)]
     emulate = args.emulate_world if world == 1 and args.emulate_world > 1 else 0
     gather = (world > 1 or emulate > 0) if args.gather is None else (args.gather and (world > 1 or emulate > 0))
+    chunks = int(args.chunks) if args.chunks != "auto" else pipeline.default_chunks(spec, n)
     if gather:
         from magical_amd import dist as mdist
         shard = mdist.ShardedVecEnv(args.env, n, rank=rank, device=str(device), gather=True,
-                                    gather_mode=args.gather_mode, emulate_world=emulate or None)
+                                    gather_mode=args.gather_mode, emulate_world=emulate or None,
+                                    window=args.restack == "window", chunks=chunks)
         vec = shard.vec
         step = shard.step_async
-    chunks = 1
-    if not gather:
-        chunks = int(args.chunks) if args.chunks != "auto" else pipeline.default_chunks(spec, n)
-    if chunks > 1:
+    if chunks > 1 and not gather:
         vec = pipeline.PipelinedVecEnv(args.env, n, chunks=chunks, device=str(device), seeds=seeds)
         step = vec.step
     elif not gather:
@@ -356,14 +377,29 @@ def main():
     t_step_ms, t_render_ms, n_timed = tm[0] / args.steps, tm[1] / args.steps, int(tm[2])
     t_reset_ms = tm[3] / args.steps
     units = n / chunks   # envs one kernel launch completes (on average over the chunks)
+    # chunked runs: the timed launches overlap the other chunk's kernels, so their HIP-event times are
+    # co-running figures.  The roofline's per-kernel times come from an isolated pass after the timed region:
+    # chunk 0 stepped alone (its step, reset and render kernels back to back on one stream, nothing beside
+    # them), args.iso_steps steps of the same env count per launch.
+    iso = None
+    if chunks > 1 and args.iso_steps > 0:
+        sim0 = vec.sims[0]
+        native.check(lib.mg_enable_timing(sim0.handle, args.iso_steps))
+        a0 = torch.empty(sim0.num_envs, dtype=torch.uint8, device=device)
+        for s in range(args.iso_steps):
+            sim0.random_actions(10 ** 6 + s, out=a0)
+            sim0.step(a0)
+        torch.cuda.synchronize(device)
+        ti = (ctypes.c_double * 4)()
+        native.check(lib.mg_read_timing(sim0.handle, ti))
+        iso = {"steps": args.iso_steps, "envs_per_launch": sim0.num_envs,
+               "step_kernel": ti[0] / args.iso_steps, "render_kernel": ti[1] / args.iso_steps,
+               "reset_kernel": ti[3] / args.iso_steps}
 
     def pmc_for(kernel):
-        """The committed PMC record of this workload; the passes run unchunked (n envs per launch), so a
-        chunked line scales its bytes per launch to the chunk's envs."""
-        rec = load_pmc(kernel, args.env, n)
-        if rec and chunks > 1 and rec.get("bytes_per_launch"):
-            rec = dict(rec, bytes_per_launch=rec["bytes_per_launch"] * units / n, scaled_from_envs=n)
-        return rec
+        """The committed PMC record of this workload at this many envs per launch (the passes run the bench's
+        own chunking; rocprofv3 counts each dispatch on its own)."""
+        return load_pmc(kernel, args.env, n, units)
     errors = int((vec.errors() != 0).sum().item())
     ranks_seen = world
     if world > 1:
@@ -375,26 +411,37 @@ def main():
         errors, ranks_seen = int(e[0].item()), int(e[1].item())
     value = world * n * args.steps / elapsed   # (--emulate-world: this rank's env-steps/s under the W-rank load)
     restack_ms = shard.restack_ms() / args.steps if gather and shard.restack_timing else None
+    exchange_ms = shard.exchange_ms() / args.steps if gather and shard.restack_timing else None
     if rank == 0:
         frames_only = gather and args.gather_mode == "frames"
+        # per-kernel roofline records: from the isolated pass when the timed launches co-ran (chunks > 1)
+        k_step, k_render, k_reset = (iso["step_kernel"], iso["render_kernel"], iso["reset_kernel"]) if iso else \
+            (t_step_ms, t_render_ms, t_reset_ms)
         kernels = {
-            "render_kernel": kernel_record("render_kernel", t_render_ms, spec.preproc, units,
+            "render_kernel": kernel_record("render_kernel", k_render, spec.preproc, units,
                                            pmc_for("render_kernel"), frames_only),
-            "step_kernel": kernel_record("step_kernel", t_step_ms, spec.preproc, units, pmc_for("step_kernel")),
-            "reset_kernel": {"ms": round(t_reset_ms, 4)},
+            "step_kernel": kernel_record("step_kernel", k_step, spec.preproc, units, pmc_for("step_kernel")),
+            "reset_kernel": {"ms": round(k_reset, 4)},
+            "timing": "isolated (chunk 0 alone after the timed region)" if iso else "timed launches (one stream)",
         }
-        dom = "render_kernel" if t_render_ms >= t_step_ms else "step_kernel"
+        dom = "render_kernel" if k_render >= k_step else "step_kernel"
         dk = kernels[dom]
+        ms_step = elapsed / args.steps * 1e3
+        # whole-step fraction: SURVEY 8(d) bytes of every env-step this GPU completes per timed step
+        step_achieved, step_frac = step_fraction(spec.preproc, n, ms_step)
         out = {
             "metric": "env-steps/sec (whole node) at N instances/GPU, 1/2/4/8 MI355X",
             "value": round(value, 1),
             "unit": "env-steps/s",
             "n_gpus": world,
             "emulated_world": emulate or None,
+            # --emulate-world W: one process stands in for rank 0 of a W-rank node; value is THIS rank's
+            # env-steps/s under the emulated exchange, not a whole-node figure
+            "value_scope": "per rank (emulated W-rank exchange on one GPU)" if emulate else "whole node",
             "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -413,6 +460,8 @@ def main():
             # binding resource of both kernels is VALU issue / latency
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": dk["achieved_gbs"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": dk["hbm_frac"], "traffic": dk["traffic_bytes_per_launch"],
+                         "kernel_timing": kernels["timing"],
+                         "step_achieved": round(step_achieved, 2), "step_frac": round(step_frac, 5),
                          "traffic_ratio": dk["traffic_ratio"],
                          "traffic_ratio_basis_bytes_per_env_step": dk["traffic_ratio_basis_bytes_per_env_step"],
                          "bytes_per_env_step": dk["bytes_per_env_step"], "units_per_launch": round(units, 1),
@@ -423,19 +472,24 @@ def main():
                          "binding": "valu_issue_latency",
                          "valu_issue_frac": dk["valu_issue_frac"], "wait_any_frac": dk["wait_any_frac"]},
             "kernels": kernels,
-            # per launch (one launch per chunk and step: chunks > 1 overlap them, so these do not add up to
-            # ms_per_step)
+            # the timed launches' HIP-event averages, per launch (one launch per chunk and step: chunks > 1 co-run
+            # them with the other chunk's kernels, so these do not add up to ms_per_step)
             "kernel_ms_per_step": {"step_kernel": round(t_step_ms, 4), "reset_kernel": round(t_reset_ms, 4),
                                    "render_kernel": round(t_render_ms, 4), "timed_launches": n_timed,
-                                   "envs_per_launch": round(units, 1)},
+                                   "envs_per_launch": round(units, 1),
+                                   "timing": "co-running (chunks overlap)" if chunks > 1 else "one stream"},
             "env_errors": errors,
             "gather": ({"mode": args.gather_mode, "ranks": shard.world, "bytes_per_rank_step": shard.layout.nbytes,
                         "stacked_bytes_per_rank_step": shard.stacked_nbytes,
                         "received_bytes_per_rank_step": (shard.world - 1) * shard.layout.nbytes,
-                        "restack_bytes_per_rank_step": (shard.world * n * restack_bytes(spec.preproc)
+                        "restack": ("window" if isinstance(shard.restacker, mdist.WindowRestacker) else "materialize")
+                                   if frames_only else None,
+                        "restack_bytes_per_rank_step": (shard.world * n * restack_bytes(
+                            spec.preproc, window=isinstance(shard.restacker, mdist.WindowRestacker))
                                                         if frames_only else 0),
                         "emulated": bool(emulate), "emulated_copy": shard.emulated_copy,
-                        "restack_ms_per_step": round(restack_ms, 4) if restack_ms is not None else None}
+                        "restack_ms_per_step": round(restack_ms, 4) if restack_ms is not None else None,
+                        "exchange_ms_per_step": round(exchange_ms, 4) if exchange_ms is not None else None}
                        if gather else None),
             "cpu_baseline": cpu,
         }

@@ -130,6 +130,20 @@ int mg_replay_lores(const uint8_t *frames, int32_t nframes, const int32_t *episo
 int mg_restack(const uint8_t *recv, int32_t world, int32_t n, int64_t rank_stride, int64_t off_allo, int64_t off_ego,
                int64_t off_done, int32_t preproc, int64_t step, int32_t all_fresh, uint8_t *ring, uint8_t *out_allo,
                uint8_t *out_ego, uint8_t *out_past, void *stream);
+/* The same stacks as a window ring (round 5): every received frame is written once, channel-planar
+ * (u8[3][96][96]), into ring u8[stacks][world*n][K + 3][3][96][96] (stacks as for mg_restack; caller-owned,
+ * persistent; K >= 4): frame t of env g goes to slot t % K, and also to slot K + t % K when t % K < 3, so for
+ * every env the frames t-3 .. t (oldest first) occupy the consecutive slots s0 .. s0 + 3, s0 = (t + K - 3) % K.
+ * The stacked output of step t is then the strided view [world*n, 96, 96, 12] of the ring at byte offset
+ * s0 * 27648 with strides (env (K + 3) * 27648, y 96, x 1, channel 9216) -- channel k of a stack = plane k % 3
+ * of its frame k / 3 -- identical to mg_restack's outputs value for value, with no stack written.  A fresh env
+ * (all_fresh, or its done flag) writes its frame into the slots of frames t-3 .. t.  preproc 1 (LoRes4E /
+ * CHW4E / CHW4A), 2 (LoResStack), 4 (LoRes4A); LoRes3EA (allo frame in front of 3 ego frames) is not a window
+ * of one ring: use mg_restack.  Step t's views stay valid until the call for step t + 1 is ordered after
+ * their readers (the ring's slot t + 1 - K ... is rewritten then; for a fresh env the slots of t-3 .. t). */
+int mg_restack_window(const uint8_t *recv, int32_t world, int32_t n, int64_t rank_stride, int64_t off_allo,
+                      int64_t off_ego, int64_t off_done, int32_t preproc, int64_t step, int32_t all_fresh, int32_t K,
+                      uint8_t *ring, void *stream);
 void mg_destroy(mg_sim *sim);
 const char *mg_last_error(void);
 

@@ -204,7 +204,77 @@ __global__ __launch_bounds__(256) void restack_kernel(const uint8_t *__restrict_
     }
 }
 
+// Receiver-side frame stacks as a window ring (mg_restack_window, round 5): instead of materialising every
+// env's [96][96][12] stack each step (read the current frame + 3 ring frames, write 1 ring frame + 4 stack
+// frames: 9 frame passes), each received frame is written once, channel-planar ([3][96][96]), into a ring of
+// K + 3 slots per env and stack: frame f goes to slot f % K, and the frames with f % K < 3 also to slot
+// K + f % K.  The 4 frames t-3 .. t then sit in the 4 consecutive slots from s0 = (t - 3) mod K on, for every
+// env, so the stack of step t is a strided view of the ring (channel k = 4-frame slot k / 3, plane k % 3:
+// channel stride 96 * 96, pixel strides 96 / 1) -- the host returns it with as_strided, no copy.  Per env-step
+// and stacked view: 1 frame read, 1 + 3 / K frames written.  A fresh env (reset, or done = auto-reset) writes
+// its frame into the slots of frames t-3 .. t (the deques of benchmarks/__init__.py:75-82,139-147 are filled
+// with the reset frame).  One thread per 16 pixels: 3 x 16 B loads of HWC bytes, 3 x 16 B planar stores
+// (consecutive lanes store consecutive 16 B of a plane: fully coalesced).
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[12], int k) { return (w[k >> 2] >> (8 * (k & 3))) & 255u; }
+
+__global__ __launch_bounds__(256) void restack_window_kernel(const uint8_t *__restrict__ recv, uint32_t world,
+                                                             uint32_t n, int64_t stride, int64_t off_a, int64_t off_e,
+                                                             int64_t off_d, int32_t preproc, int64_t step,
+                                                             int32_t all_fresh, uint32_t K, uint8_t *__restrict__ ring) {
+    constexpr uint32_t PL = LO * LO;          // bytes of one colour plane
+    constexpr uint32_t Q = PL / 16;           // 16-pixel groups per frame
+    const uint32_t WN = world * n;
+    const int s = blockIdx.y;                 // output stack (LoResStack: 0 allo / 1 ego; else 0)
+    const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
+    if (gid >= WN * Q) return;
+    const uint32_t g = gid / Q, q = gid - g * Q;
+    const uint32_t r = g / n, i = g - r * n;
+    const uint8_t *blk = recv + (size_t)r * stride;
+    const bool fresh = all_fresh || blk[off_d + i] != 0;
+    const int rv = (preproc == MG_PREPROC_LORES4A || (preproc == MG_PREPROC_LORESSTACK && s == 0)) ? 0 : 1;
+    const uint4 *cur = (const uint4 *)(blk + (rv ? off_e : off_a) + (size_t)i * LOFR + (size_t)q * 48);
+    uint32_t w[12];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint4 v = cur[k];
+        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+    uint4 pl[3];                              // plane c, pixels 16q .. 16q + 15
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        uint32_t o[4];
+#pragma unroll
+        for (int d = 0; d < 4; d++)
+            o[d] = byte_of(w, 3 * (4 * d) + c) | byte_of(w, 3 * (4 * d + 1) + c) << 8 |
+                   byte_of(w, 3 * (4 * d + 2) + c) << 16 | byte_of(w, 3 * (4 * d + 3) + c) << 24;
+        pl[c] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    uint8_t *env_ring = ring + ((size_t)s * WN + g) * (K + 3) * LOFR + (size_t)q * 16;
+    auto put = [&](uint32_t slot) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) *(uint4 *)(env_ring + (size_t)slot * LOFR + (size_t)c * PL) = pl[c];
+    };
+    const uint32_t p = (uint32_t)(step % K);
+    for (uint32_t j = 0; j < (fresh ? 4u : 1u); j++) {   // frames t, t-1, t-2, t-3 (fresh: all four slots)
+        const uint32_t f = (p + K - j) % K;
+        put(f);
+        if (f < 3) put(K + f);
+    }
+}
+
 }  // namespace
+
+extern "C" hipError_t mg_launch_restack_window(const uint8_t *recv, int32_t world, int32_t n, int64_t stride,
+                                               int64_t off_a, int64_t off_e, int64_t off_d, int32_t preproc,
+                                               int64_t step, int32_t all_fresh, int32_t K, uint8_t *ring,
+                                               hipStream_t st) {
+    const int64_t t = (int64_t)world * n * (LO * LO / 16);
+    const bool two = preproc == MG_PREPROC_LORESSTACK;
+    hipLaunchKernelGGL(restack_window_kernel, dim3((unsigned)((t + 255) / 256), two ? 2 : 1), dim3(256), 0, st, recv,
+                       (uint32_t)world, (uint32_t)n, stride, off_a, off_e, off_d, preproc, step, all_fresh,
+                       (uint32_t)K, ring);
+    return hipGetLastError();
+}
 
 // launcher, C linkage (declared in mg_sim.hip next to the ABI entry mg_replay_lores)
 extern "C" hipError_t mg_launch_replay(const uint8_t *frames, int32_t nframes, const int32_t *episode_start,

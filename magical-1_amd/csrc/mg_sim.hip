@@ -561,6 +561,32 @@ int mg_restack(const uint8_t *recv, int32_t world, int32_t n, int64_t rank_strid
     return 0;
 }
 
+hipError_t mg_launch_restack_window(const uint8_t *recv, int32_t world, int32_t n, int64_t stride, int64_t off_a,
+                                    int64_t off_e, int64_t off_d, int32_t preproc, int64_t step, int32_t all_fresh,
+                                    int32_t K, uint8_t *ring, hipStream_t st);
+
+int mg_restack_window(const uint8_t *recv, int32_t world, int32_t n, int64_t rank_stride, int64_t off_allo,
+                      int64_t off_ego, int64_t off_done, int32_t preproc, int64_t step, int32_t all_fresh, int32_t K,
+                      uint8_t *ring, void *stream) {
+    if (!recv || !ring || world <= 0 || n <= 0 || step < 0) return set_err(-22, "mg_restack_window: null argument or bad size");
+    if (K < 4 || K > 64) return set_err(-22, "mg_restack_window: K must be in [4, 64]");
+    if (preproc != MG_PREPROC_LORES4E && preproc != MG_PREPROC_LORESSTACK && preproc != MG_PREPROC_LORES4A)
+        return set_err(-22, "mg_restack_window: preproc must be 1 (LoRes4E), 2 (LoResStack) or 4 (LoRes4A); "
+                            "LoRes3EA's stack is not one ring's window (use mg_restack)");
+    if ((int64_t)world * n * (MG_LORES * MG_LORES / 16) >= ((int64_t)1 << 31))
+        return set_err(-22, "mg_restack_window: world * n too large for one launch");
+    const int64_t FR = (int64_t)MG_LORES * MG_LORES * 3;
+    if (off_allo < 0 || off_ego < 0 || off_done < 0 || off_allo + n * FR > rank_stride || off_ego + n * FR > rank_stride ||
+        off_done + n > rank_stride)
+        return set_err(-22, "mg_restack_window: a key of the rank block lies outside rank_stride");
+    const int64_t al[5] = {(int64_t)(uintptr_t)recv, rank_stride, off_allo, off_ego, (int64_t)(uintptr_t)ring};
+    for (int64_t a : al)
+        if (a & 15) return set_err(-22, "mg_restack_window: recv, ring, rank_stride and frame offsets must be 16-byte aligned");
+    HIPC(mg_launch_restack_window(recv, world, n, rank_stride, off_allo, off_ego, off_done, preproc, step, all_fresh, K,
+                                  ring, as_stream(stream)));
+    return 0;
+}
+
 int mg_render_full(mg_sim *s, uint8_t *out, void *stream) {
     if (!s || !out) return set_err(-22, "mg_render_full: null argument");
     HIPC(hipSetDevice(s->device));

@@ -17,18 +17,29 @@ the whole node's step results -- is one all-gather per step:
   LoRes frame of each view plus reward / done / eval_score[, target] -- 55 312
   B per env instead of 165 904 (LoRes4E) or 221 200 (LoResStack) -- because 3
   of every 4 stacked frames already reached every rank in earlier steps.  Each
-  receiver rebuilds the frame stacks of all W * n envs from a ring of their
-  last 4 frames (mg_restack, a HIP kernel; the reset frame fills every slot as
-  in benchmarks/__init__.py:75-82,139-147, and an env whose done flag is set
-  restarts its stacks: its frame is the next episode's first).  The simulator
+  receiver keeps the frame stacks of all W * n envs as a window ring
+  (WindowRestacker, mg_restack_window, round 5): every received frame is
+  written once, channel-planar, into a ring of K + 3 slots per env, and the
+  stack of step t is a strided view of 4 consecutive slots -- 1 frame read and
+  ~1.4 written per env and stacked view instead of materialising the stack (9
+  frame passes; NativeRestacker, mg_restack, still used for LoRes3EA, whose
+  stack is not one ring's window).  The reset frame fills every slot as in
+  benchmarks/__init__.py:75-82,139-147, and an env whose done flag is set
+  restarts its stacks (its frame is the next episode's first).  The simulator
   binds its outputs in frames-only mode, so it writes no stacks of its own.
   gather_mode "stacked" gathers the preprocessor's whole outputs instead;
 * `nbuf` buffer sets (default 3) rotate between steps; the collective runs on its
   own HIP stream and the restack on a third (in step order), so the exchange of
   step t overlaps the compute of steps t + 1 .. t + nbuf - 1 and the restack of
   step t (HBM-bound) overlaps the all-gather of step t + 1 (xGMI-bound)
-  (ShardedVecEnv.step_async).  A step's gathered views stay valid for the next
-  nbuf - 1 steps.
+  (ShardedVecEnv.step_async).  A step's gathered frames, rewards, done flags and
+  scores stay valid for the next nbuf - 1 steps; its stacked views (window
+  ring) until the next step_async() / reset_async() -- work the caller queued
+  on its stream before that call is ordered before the ring is rewritten (as a
+  VecMagicalEnv's outputs are valid until its next step).
+* the env underneath may be a magical_amd.pipeline.PipelinedVecEnv (chunks > 1):
+  the collective then waits for every chunk's stream of the step, so the chunks
+  keep overlapping one another's kernels under the exchange.
 """
 import collections
 
@@ -140,10 +151,33 @@ def restack_ring_bytes(preproc, world, n):
     return len(stacked_keys(preproc)) * 4 * world * n * LOFR
 
 
+WINDOW_K = 8   # window ring period: K + 3 slots per env and stack, 3 / K extra frame writes per step
+
+
+def window_ring_bytes(preproc, world, n, K=WINDOW_K):
+    """Bytes of mg_restack_window's ring: u8[stacks][W * n][K + 3][3][96][96]."""
+    return len(stacked_keys(preproc)) * world * n * (K + 3) * LOFR
+
+
+def uses_window(preproc):
+    """The stacks of these preprocessors are windows of one ring (LoRes3EA's is not: allo frame + 3 ego)."""
+    return preproc != "LoRes3EA"
+
+
 def frames_mode_bytes(preproc, world, n, nbuf=3):
-    """Receiver-side device memory of gather_mode 'frames' per rank: the ring plus nbuf sets of rebuilt
-    stacks (u8[W * n][96][96][12] per stacked key, one set per rotating buffer set)."""
+    """Receiver-side device memory of gather_mode 'frames' per rank: the window ring (LoRes3EA: mg_restack's
+    ring plus nbuf sets of rebuilt stacks, u8[W * n][96][96][12] per set)."""
+    if uses_window(preproc):
+        return window_ring_bytes(preproc, world, n)
     return restack_ring_bytes(preproc, world, n) + nbuf * len(stacked_keys(preproc)) * world * n * 4 * LOFR
+
+
+def window_view(ring, k, wn, s0, K=WINDOW_K):
+    """Stack k's [wn, 96, 96, 12] view of the window ring at window start slot s0 (include/magical_sim.h
+    mg_restack_window): channel c = plane c % 3 of slot s0 + c // 3."""
+    plane = 96 * 96
+    return ring.as_strided((wn, 96, 96, 12), ((K + 3) * LOFR, 96, 1, plane),
+                           ring.storage_offset() + (k * wn * (K + 3) + s0) * LOFR)
 
 
 _HIP = None
@@ -176,7 +210,11 @@ def _emulate_all_gather(recv, send, world, stream):
 
 class NativeRestacker:
     """Receiver-side frame stacks of the frames-only gather on the GPU (mg_restack): keeps a ring of the
-    last 4 frames of each stacked output's view for all W * n envs (restack_ring_bytes)."""
+    last 4 frames of each stacked output's view for all W * n envs (restack_ring_bytes) and writes every
+    step's stacks into `outs` (materialised: 9 frame passes per env and stack; LoRes3EA, and the contiguous
+    reference the window ring is tested against)."""
+
+    materialized = True
 
     def __init__(self, layout, world, device):
         from . import native
@@ -195,6 +233,38 @@ class NativeRestacker:
             p(recv), self.world, self.layout.n, self.layout.nbytes, self.off[0], self.off[1], self.off[2],
             self.preproc, int(step), 1 if all_fresh else 0, p(self.ring), p(outs.get("allo")), p(outs.get("ego")),
             p(outs.get("past_obs")), st))
+
+
+class WindowRestacker:
+    """Receiver-side frame stacks of the frames-only gather as a window ring on the GPU (mg_restack_window):
+    __call__ returns the step's stacks as strided views of the ring (valid until the next call is ordered
+    after their readers); nothing is materialised."""
+
+    materialized = False
+
+    def __init__(self, layout, world, device, K=WINDOW_K):
+        from . import native
+        if not uses_window(layout.preproc):
+            raise ValueError(f"{layout.preproc}: the stack is not a window of one ring (use NativeRestacker)")
+        self.lib, self.native = native.load(), native
+        self.layout, self.world, self.K = layout, world, int(K)
+        self.preproc = GPU_PREPROC[layout.preproc]
+        self.keys = stacked_keys(layout.preproc)
+        self.wn = world * layout.n
+        self.ring = torch.empty(window_ring_bytes(layout.preproc, world, layout.n, self.K), dtype=torch.uint8,
+                                device=device)
+        self.off = (layout.offset("allo"), layout.offset("ego"), layout.offset("done"))
+
+    def __call__(self, recv, outs, step, all_fresh):
+        import ctypes
+        st = ctypes.c_void_p(torch.cuda.current_stream(recv.device).cuda_stream)
+        self.native.check(self.lib.mg_restack_window(
+            ctypes.c_void_p(recv.data_ptr()), self.world, self.layout.n, self.layout.nbytes, self.off[0], self.off[1],
+            self.off[2], self.preproc, int(step), 1 if all_fresh else 0, self.K, ctypes.c_void_p(self.ring.data_ptr()),
+            st))
+        s0 = (int(step) + self.K - 3) % self.K
+        return collections.OrderedDict((k, window_view(self.ring, j, self.wn, s0, self.K))
+                                       for j, k in enumerate(self.keys))
 
 
 class GatheredStep:
@@ -249,7 +319,8 @@ class ShardedVecEnv:
     reset directly (vec.reset()), since the other ranks' rings would then hold stale frames of its envs."""
 
     def __init__(self, env_name, envs_per_rank, rank=None, device=None, base_seed=1000, gather=False, vec=None,
-                 gather_mode=None, restacker=None, max_episode_steps=None, emulate_world=None, nbuf=3):
+                 gather_mode=None, restacker=None, max_episode_steps=None, emulate_world=None, nbuf=3, window=True,
+                 chunks=1):
         from . import registry
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if dist.is_initialized() else 1
@@ -265,10 +336,19 @@ class ShardedVecEnv:
         self.gather = gather
         spec = registry.lookup(env_name)
         if vec is None:
-            from .envs import VecMagicalEnv
-            vec = VecMagicalEnv(env_name, envs_per_rank, device=device or f"cuda:{torch.cuda.current_device()}",
-                                seeds=shard_seeds(envs_per_rank, self.rank, base_seed),
-                                max_episode_steps=max_episode_steps)
+            dev_name = device or f"cuda:{torch.cuda.current_device()}"
+            seeds = shard_seeds(envs_per_rank, self.rank, base_seed)
+            if chunks > 1:   # the pipelined env pool (magical_amd.pipeline): chunks overlap under the exchange
+                if spec.task == "PickAndPlace":
+                    raise ValueError("ShardedVecEnv: a pipelined PickAndPlace shard would gather its target before "
+                                     "the chunks' resets wrote it")
+                from .pipeline import PipelinedVecEnv
+                vec = PipelinedVecEnv(env_name, envs_per_rank, chunks=chunks, device=dev_name, seeds=seeds,
+                                      max_episode_steps=max_episode_steps)
+            else:
+                from .envs import VecMagicalEnv
+                vec = VecMagicalEnv(env_name, envs_per_rank, device=dev_name, seeds=seeds,
+                                    max_episode_steps=max_episode_steps)
         self.vec = vec
         if gather:
             dev = torch.device(device) if device is not None else getattr(vec, "device", torch.device("cpu"))
@@ -290,13 +370,17 @@ class ShardedVecEnv:
             self.recv = [torch.empty(self.world * self.layout.nbytes, dtype=torch.uint8, device=dev) for _ in range(nb)]
             self.stacks = [None] * nb
             if frames:
-                wn = self.world * envs_per_rank
-                self.stacks = [collections.OrderedDict((k, torch.empty((wn, 96, 96, 12), dtype=torch.uint8, device=dev))
-                                                       for k in stacked_keys(spec.preproc)) for _ in range(nb)]
                 if restacker is None:
                     if dev.type != "cuda":
                         raise ValueError("gather_mode 'frames' on CPU tensors needs a restacker")
-                    restacker = NativeRestacker(self.layout, self.world, dev)
+                    restacker = (WindowRestacker(self.layout, self.world, dev) if uses_window(spec.preproc) and
+                                 window else NativeRestacker(self.layout, self.world, dev))
+                wn = self.world * envs_per_rank
+                # materialised stacks (mg_restack, the oracle's restacker): one set per buffer set; the window
+                # ring's views need none
+                self.stacks = [collections.OrderedDict((k, torch.empty((wn, 96, 96, 12), dtype=torch.uint8, device=dev))
+                                                       for k in stacked_keys(spec.preproc))
+                               if getattr(restacker, "materialized", True) else {} for _ in range(nb)]
             self.restacker = restacker
             self.pending = [None] * nb
             self.comm_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
@@ -310,17 +394,28 @@ class ShardedVecEnv:
             self._restack_ev = []
 
     def enable_restack_timing(self):
-        """time every following restack with HIP events on the restack stream (bench.py)"""
+        """time every following exchange (on the comm stream) and restack (on the restack stream) with HIP
+        events (bench.py)"""
         self.restack_timing = self.restack_stream is not None
         self._restack_ev = []
+        self._comm_ev = []
 
-    def restack_ms(self):
-        """total ms of the restacks timed since enable_restack_timing (synchronises on the last one)"""
+    @staticmethod
+    def _total_ms(pairs):
         tot = 0.0
-        for a, b in self._restack_ev:
+        for a, b in pairs:
             b.synchronize()
             tot += a.elapsed_time(b)
         return tot
+
+    def restack_ms(self):
+        """total ms of the restacks timed since enable_restack_timing (synchronises on the last one)"""
+        return self._total_ms(self._restack_ev)
+
+    def exchange_ms(self):
+        """total ms of the all-gathers (or their --emulate-world copies) on the comm stream, from the collective's
+        first operation to its last (the wait for the step's compute is not counted)"""
+        return self._total_ms(getattr(self, "_comm_ev", []))
 
     # -- packed gather pipeline ---------------------------------------------------------------------------
     def _begin(self):
@@ -345,13 +440,22 @@ class ShardedVecEnv:
             ev = torch.cuda.current_stream(self.device).record_event()
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
+                for cev in getattr(self.vec, "step_events", lambda: [])():   # a pipelined pool's chunk streams
+                    self.comm_stream.wait_event(cev)
                 if self.restacked[b] is not None:   # the restack of step t - 2 has read recv[b]
                     self.comm_stream.wait_event(self.restacked[b])
+                if self.restack_timing:
+                    c0 = torch.cuda.Event(enable_timing=True)
+                    c0.record(self.comm_stream)
                 if self.emulate_world:
                     self.emulated_copy = _emulate_all_gather(recv, send, self.world, self.comm_stream)
                 else:
                     work = dist.all_gather_into_tensor(recv, send, async_op=True)
                     work.wait()   # the side stream (not the host) waits for the collective
+                if self.restack_timing:
+                    c1 = torch.cuda.Event(enable_timing=True)
+                    c1.record(self.comm_stream)
+                    self._comm_ev.append((c0, c1))
                 done_ev = self.comm_stream.record_event()
             if stacks is not None:
                 # in step order on its own stream (the receive ring carries state from step to step)
@@ -360,7 +464,7 @@ class ShardedVecEnv:
                     if self.restack_timing:
                         t0 = torch.cuda.Event(enable_timing=True)
                         t0.record(self.restack_stream)
-                    self.restacker(recv, stacks, step, all_fresh)
+                    stacks = self.restacker(recv, stacks, step, all_fresh) or stacks
                     if self.restack_timing:
                         t1 = torch.cuda.Event(enable_timing=True)
                         t1.record(self.restack_stream)
@@ -371,7 +475,7 @@ class ShardedVecEnv:
             work = dist.all_gather_into_tensor(recv, send, async_op=True)
             work.wait()
             if stacks is not None:
-                self.restacker(recv, stacks, step, all_fresh)
+                stacks = self.restacker(recv, stacks, step, all_fresh) or stacks
             h = GatheredStep(self.layout, recv, stacks)
         self.pending[b] = h
         self.t += 1

@@ -74,6 +74,9 @@ class PipelinedVecEnv:
         # done[k][slot]: chunk k finished the step that read action slot `slot`
         self.done_ev = [[None, None] for _ in range(chunks)]
         self.t = 0
+        self.reset_count = 0      # explicit reset() calls (magical_amd.dist checks its frame rings against it)
+        self.target = self.buffers.get("target")
+        self._last = []           # the chunk streams' events of the last step() (magical_amd.dist waits on them)
 
     # -- ordering ------------------------------------------------------------------
     def _caller(self):
@@ -94,11 +97,28 @@ class PipelinedVecEnv:
             ev.record(self.streams[k])
             cs.wait_event(ev)
 
+    def step_events(self):
+        """Events recorded on every chunk's stream after its last step() (a consumer on another stream, e.g.
+        magical_amd.dist's collective, waits on them instead of ordering the caller's stream after the chunks,
+        which would make the next step's chunks wait for each other)."""
+        return list(self._last)
+
+    def bind_outputs(self, views, frames_only=False):
+        """Bind full-batch [num_envs, ...] output views (VecMagicalEnv.bind_outputs keys): chunk k writes rows
+        [bounds[k], bounds[k + 1]) of each.  Called between steps (magical_amd.dist binds a packed buffer set per
+        step); the chunks' streams are ordered after the caller's stream by the next step()'s fork."""
+        b = self.bounds
+        for k, sim in enumerate(self.sims):
+            sim.bind_outputs({key: v[b[k]:b[k + 1]] for key, v in views.items() if key != "target"},
+                             frames_only=frames_only)
+
     # -- API -----------------------------------------------------------------------
     def reset(self, mask=None):
         self.wait()
         for k, sim in enumerate(self.sims):
             sim.reset(None if mask is None else mask[self.bounds[k]:self.bounds[k + 1]])
+        self.reset_count += 1
+        self._last = []
         self._fork()
         return self._obs()
 
@@ -120,6 +140,7 @@ class PipelinedVecEnv:
             ev = torch.cuda.Event()
             ev.record(st)
             self.done_ev[k][slot] = ev
+        self._last = [self.done_ev[k][slot] for k in range(self.chunks)]
         self.t += 1
         return self._obs(), self.buffers["reward"], self.buffers["done"], {"eval_score": self.buffers["eval_score"]}
 

@@ -805,22 +805,37 @@ def test_layout_retry_parity(name, tries, monkeypatch):
     vec.close()
 
 
-GATHER_GPU_CASES = [("MoveToRegion-Demo-LoRes4E-v0", "frames", 40), ("MoveToRegion-Demo-LoRes4E-v0", "stacked", 40),
-                    ("MoveToRegion-Demo-LoResCHW4E-v0", "frames", 40), ("ClusterColour-Demo-LoResStack-v0", "frames", 12),
-                    ("ClusterColour-Demo-LoResStack-v0", "stacked", 12), ("MoveToCorner-Demo-LoRes3EA-v0", "frames", 15),
-                    ("MoveToCorner-Demo-LoRes4A-v0", "frames", 15), ("PickAndPlace-Demo-LoRes4E-v0", "frames", 15)]
+# (name, gather mode, episode length, options): frames mode keeps the stacks as window-ring views (mg_restack_window,
+# valid until the next step_async) except LoRes3EA and window=False (materialised by mg_restack, valid for nbuf - 1
+# steps); chunks=2 runs the shard as a pipelined env pool under the exchange
+GATHER_GPU_CASES = [("MoveToRegion-Demo-LoRes4E-v0", "frames", 40, {}),
+                    ("MoveToRegion-Demo-LoRes4E-v0", "frames", 40, {"window": False}),
+                    ("MoveToRegion-Demo-LoRes4E-v0", "frames", 40, {"chunks": 2}),
+                    ("MoveToRegion-Demo-LoRes4E-v0", "stacked", 40, {}),
+                    ("MoveToRegion-Demo-LoResCHW4E-v0", "frames", 40, {}),
+                    ("ClusterColour-Demo-LoResStack-v0", "frames", 12, {}),
+                    ("ClusterColour-Demo-LoResStack-v0", "frames", 12, {"window": False}),
+                    ("ClusterColour-Demo-LoResStack-v0", "stacked", 12, {}),
+                    ("MoveToCorner-Demo-LoRes3EA-v0", "frames", 15, {}),
+                    ("MoveToCorner-Demo-LoRes4A-v0", "frames", 15, {}),
+                    ("MoveToCorner-Demo-LoRes4A-v0", "frames", 15, {"chunks": 2}),
+                    ("PickAndPlace-Demo-LoRes4E-v0", "frames", 15, {})]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,mode,L", GATHER_GPU_CASES)
-def test_packed_gather_pipeline_single_rank(tmp_path, name, mode, L):
+@pytest.mark.parametrize("name,mode,L,opts", GATHER_GPU_CASES,
+                         ids=[f"{c[0].split('-')[0]}-{c[0].split('-')[2]}-{c[1]}-" + "-".join(f"{k}{v}" for k, v in c[3].items())
+                              for c in GATHER_GPU_CASES])
+def test_packed_gather_pipeline_single_rank(tmp_path, name, mode, L, opts):
     """The multi-GPU exchange path on one GPU (a 1-rank RCCL group): the simulator writes each step's
     outputs straight into views of a packed buffer (bind_outputs; gather_mode 'frames': the current frames
     only), one all_gather_into_tensor per step on a side stream, then (frames) the receiver-side restack
-    kernel mg_restack rebuilds the frame stacks; two buffer sets alternate.  Every step's gathered
-    [1, n, ...] results equal a plain VecMagicalEnv run bit for bit (obs incl. the rebuilt stacks and the
-    CHW views, reward, done, eval_score, PickAndPlace's target), over 45 steps that cross auto-resets
-    (episode length L)."""
+    (window ring views, or mg_restack's materialised stacks) rebuilds the frame stacks; three buffer sets
+    rotate.  Every step's gathered [1, n, ...] results equal a plain VecMagicalEnv run bit for bit (obs incl.
+    the rebuilt stacks and the CHW views, reward, done, eval_score, PickAndPlace's target), over 45 steps that
+    cross auto-resets (episode length L).  Results are read one step late (after the next step was launched)
+    where the contract allows it -- materialised stacks and the stacked mode -- and before the next step for
+    window-ring views."""
     import torch.distributed as dist
     from magical_amd import dist as mdist
     n, steps = 70, 45
@@ -828,7 +843,10 @@ def test_packed_gather_pipeline_single_rank(tmp_path, name, mode, L):
                             device_id=torch.device("cuda", 0))
     try:
         shard = mdist.ShardedVecEnv(name, n, rank=0, device="cuda:0", gather=True, gather_mode=mode,
-                                    max_episode_steps=L)
+                                    max_episode_steps=L, **opts)
+        window = isinstance(getattr(shard, "restacker", None), mdist.WindowRestacker)
+        assert window == (mode == "frames" and opts.get("window", True) and "3EA" not in name)
+        lag = 0 if window else 1
         ref = magical_amd.make_vec(name, n, seeds=mdist.shard_seeds(n, 0), max_episode_steps=L)
         acts = np.random.RandomState(4).randint(0, 18, (steps, n))
         got = shard.reset()
@@ -836,28 +854,67 @@ def test_packed_gather_pipeline_single_rank(tmp_path, name, mode, L):
         assert list(got) == list(want)
         for k in want:
             assert torch.equal(got[k][0], want[k]), f"reset {k}"
-        handles, resets = [], 0
+        handles, resets, prev = [], 0, {}
         for t in range(steps):
             a = torch.as_tensor(acts[t], dtype=torch.uint8)
             handles.append(shard.step_async(a))
             obs, rew, done, info = ref.step(a)
             resets += int(done.sum().item())
-            if t >= 1:   # the previous step's exchange, read after this step was launched
-                g_obs, g_rew, g_done, g_info = handles[t - 1].results()
-                assert list(g_obs) == list(prev[0])
-                for k in prev[0]:
-                    assert torch.equal(g_obs[k][0], prev[0][k]), f"step {t - 1} {k}"
-                assert torch.equal(g_rew[0], prev[1]) and torch.equal(g_done[0], prev[2])
-                assert torch.equal(g_info["eval_score"][0], prev[3])
+            prev[t] = ({k: v.clone() for k, v in obs.items()}, rew.clone(), done.clone(), info["eval_score"].clone(),
+                       ref.target.clone() if ref.target is not None else None)
+            u = t - lag
+            if u >= 0:
+                g_obs, g_rew, g_done, g_info = handles[u].results()
+                w = prev.pop(u)
+                assert list(g_obs) == list(w[0])
+                for k in w[0]:
+                    assert torch.equal(g_obs[k][0], w[0][k]), f"step {u} {k}"
+                assert torch.equal(g_rew[0], w[1]) and torch.equal(g_done[0], w[2])
+                assert torch.equal(g_info["eval_score"][0], w[3])
                 if "target" in g_info:
-                    assert torch.equal(g_info["target"][0], prev[4]), f"step {t - 1} target"
-            prev = ({k: v.clone() for k, v in obs.items()}, rew.clone(), done.clone(), info["eval_score"].clone(),
-                    ref.target.clone() if ref.target is not None else None)
+                    assert torch.equal(g_info["target"][0], w[4]), f"step {u} target"
         assert resets >= n * (steps // L - 1)
         shard.close()
         ref.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("preproc", ["LoRes4E", "LoResStack", "LoRes4A"])
+def test_restack_window_matches_oracle_rule(preproc):
+    """mg_restack_window on synthetic gathered batches (world 3, 37 envs per rank) with random frames and random
+    done flags over 22 steps (the window ring's K = 8 wraps twice; its duplicate slots in use), an all-fresh reset
+    first and again in the middle: the strided views equal the oracle's restatement of the reference's
+    frame-stack rule and mg_restack's materialised stacks bit for bit."""
+    from magical_amd import dist as mdist, registry
+    name = {"LoRes4E": "MoveToRegion-Demo-LoRes4E-v0", "LoResStack": "ClusterColour-Demo-LoResStack-v0",
+            "LoRes4A": "MoveToRegion-Demo-LoRes4A-v0"}[preproc]
+    spec = registry.lookup(name)
+    W, n = 3, 37
+    lay = mdist.PackedLayout.for_spec(spec, n, frames_only=True)
+    win = mdist.WindowRestacker(lay, W, torch.device("cuda", 0))
+    nat = mdist.NativeRestacker(lay, W, torch.device("cuda", 0))
+    orc = po.OracleRestacker(lay, preproc)
+    rs = np.random.RandomState(12)
+    keys = mdist.stacked_keys(preproc)
+    for t in range(22):
+        recv = torch.from_numpy(rs.randint(0, 256, W * lay.nbytes).astype(np.uint8))
+        v = lay.unpack(recv)
+        v["done"].copy_(torch.from_numpy(rs.rand(W, n) < 0.15))
+        fresh = t in (0, 13)
+        out_c = {k: torch.zeros((W * n, 96, 96, 12), dtype=torch.uint8) for k in keys}
+        out_m = {k: torch.zeros((W * n, 96, 96, 12), dtype=torch.uint8, device="cuda") for k in keys}
+        orc(recv, out_c, t, fresh)
+        rg = recv.cuda()
+        nat(rg, out_m, t, fresh)
+        views = win(rg, None, t, fresh)
+        torch.cuda.synchronize()
+        assert list(views) == list(keys)
+        for k in keys:
+            assert views[k].shape == (W * n, 96, 96, 12) and views[k].stride() == ((8 + 3) * 27648, 96, 1, 9216)
+            assert torch.equal(views[k].cpu(), out_c[k]), (t, k)
+            assert torch.equal(views[k], out_m[k]), (t, k)
 
 
 @pytest.mark.gpu
