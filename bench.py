@@ -59,14 +59,18 @@ def obs_bytes(preproc):
             "LoResStack": 221184}.get(preproc, 2 * 384 * 384 * 3)
 
 
-def render_bytes(preproc, frames_only=False):
+def render_bytes(preproc, frames_only=False, window=False, K=8):
     """Bytes the render kernel must move per env-step: the observation outputs, plus the frame ring of
     each stacked view (3 earlier frames read, the current one written; the 4 slots are filled at reset).
     frames_only (compact multi-GPU gather): the two current frames only -- the stacks are rebuilt by
-    mg_restack on the receivers."""
+    mg_restack on the receivers.  window (mg_bind_window): each stacked view writes its current frame once
+    into its window ring (+ 3 / K for the duplicate slots) instead of stack + ring, plus the plain frames."""
     if frames_only:
         return 2 * FR
     stacked_views = {"LoResStack": 2, "LoRes4E": 1, "LoRes4A": 1, "LoResCHW4E": 1, "LoResCHW4A": 1}.get(preproc, 0)
+    if window and stacked_views:
+        plain = 0 if preproc == "LoResStack" else 2 * FR
+        return int(round(plain + stacked_views * (1 + 3 / K) * FR))
     ring = stacked_views * 4 * FR
     if preproc == "LoRes3EA":   # ego ring (1 write) + compose pass (allo + 3 ring frames read, 4 frames written)
         ring = FR + 4 * FR + 4 * FR
@@ -205,7 +209,7 @@ def launch_ranks(n):
     return subprocess.call(cmd, env=dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1")))
 
 
-def kernel_record(name, ms, preproc, n, pmc, frames_only=False):
+def kernel_record(name, ms, preproc, n, pmc, frames_only=False, window=False):
     """One kernel's roofline figures over its HIP-event average duration (ms per launch, one launch per step):
     * achieved / hbm_frac: SURVEY 8(d) bytes of the env-steps the launch completes (survey_bytes x n);
     * traffic_ratio: PMC HBM bytes per launch (committed rocprofv3 FETCH/WRITE passes of the same workload
@@ -216,7 +220,7 @@ def kernel_record(name, ms, preproc, n, pmc, frames_only=False):
         return None
     sb = survey_bytes(preproc)
     ach = sb * n / (ms * 1e-3) / 1e9
-    kb = render_bytes(preproc, frames_only) if name == "render_kernel" else STATE_BYTES
+    kb = render_bytes(preproc, frames_only, window) if name == "render_kernel" else STATE_BYTES
     kach = kb * n / (ms * 1e-3) / 1e9
     traffic = pmc and pmc.get("bytes_per_launch")
     share = kernel_survey_bytes(name, preproc)
@@ -259,6 +263,9 @@ def main():
     ap.add_argument("--iso-steps", type=int, default=20,
                     help="chunked runs: steps of chunk 0 alone after the timed region, for the roofline's isolated "
                          "per-kernel times (0: none)")
+    ap.add_argument("--stacks", default="window", choices=("window", "materialize"),
+                    help="the simulator's frame stacks: strided views of window rings (mg_bind_window, default) or "
+                         "materialised [N, 96, 96, 12] tensors")
     ap.add_argument("--restack", default="window", choices=("window", "materialize"),
                     help="frames-mode receivers: window ring views (mg_restack_window) or materialised stacks "
                          "(mg_restack)")
@@ -322,11 +329,12 @@ def main():
                                     window=args.restack == "window", chunks=chunks)
         vec = shard.vec
         step = shard.step_async
+    window = args.stacks == "window"
     if chunks > 1 and not gather:
-        vec = pipeline.PipelinedVecEnv(args.env, n, chunks=chunks, device=str(device), seeds=seeds)
+        vec = pipeline.PipelinedVecEnv(args.env, n, chunks=chunks, device=str(device), seeds=seeds, window=window)
         step = vec.step
     elif not gather:
-        vec = magical_amd.make_vec(args.env, n, device=str(device), seeds=seeds)
+        vec = magical_amd.make_vec(args.env, n, device=str(device), seeds=seeds, window=window)
         step = vec.step
     lib = vec.lib
     actions = torch.empty(n, dtype=torch.uint8, device=device)
@@ -414,12 +422,13 @@ def main():
     exchange_ms = shard.exchange_ms() / args.steps if gather and shard.restack_timing else None
     if rank == 0:
         frames_only = gather and args.gather_mode == "frames"
+        stacks_window = bool(getattr(vec, "window_k", 0)) and not gather
         # per-kernel roofline records: from the isolated pass when the timed launches co-ran (chunks > 1)
         k_step, k_render, k_reset = (iso["step_kernel"], iso["render_kernel"], iso["reset_kernel"]) if iso else \
             (t_step_ms, t_render_ms, t_reset_ms)
         kernels = {
             "render_kernel": kernel_record("render_kernel", k_render, spec.preproc, units,
-                                           pmc_for("render_kernel"), frames_only),
+                                           pmc_for("render_kernel"), frames_only, stacks_window),
             "step_kernel": kernel_record("step_kernel", k_step, spec.preproc, units, pmc_for("step_kernel")),
             "reset_kernel": {"ms": round(k_reset, 4)},
             "timing": "isolated (chunk 0 alone after the timed region)" if iso else "timed launches (one stream)",
@@ -451,6 +460,11 @@ def main():
                        "physics_substeps": 10, "solver_iterations": 10, "render": "2 x 384^2 -> 96^2",
                        "phase_spread": phase_spread,
                        "pipeline_chunks": chunks,
+                       "frame_stacks": ("strided views of channel-planar window rings (mg_bind_window)"
+                                        if stacks_window else "materialised [N, 96, 96, 12]" if not gather else
+                                        "receivers: " + ("window rings" if isinstance(getattr(shard, "restacker", None),
+                                                                                   mdist.WindowRestacker) else
+                                                         "materialised")),
                        "parallelism": (f"dp{world} (envs sharded; one packed all-gather per step ({args.gather_mode}), "
                                        f"pipelined with the next step)" if gather else
                                        f"dp{world} (envs sharded, no data-path collective)")},

@@ -144,6 +144,19 @@ int mg_restack(const uint8_t *recv, int32_t world, int32_t n, int64_t rank_strid
 int mg_restack_window(const uint8_t *recv, int32_t world, int32_t n, int64_t rank_stride, int64_t off_allo,
                       int64_t off_ego, int64_t off_done, int32_t preproc, int64_t step, int32_t all_fresh, int32_t K,
                       uint8_t *ring, void *stream);
+/* Stacked outputs as window rings on the simulator itself (round 5).  ring_allo / ring_ego: device
+ * u8[num_envs][K + 3][3][96][96], caller-owned, 16-byte aligned, one for each stacked view of the preprocessor
+ * (LoResStack: allo and ego; LoRes4E / CHW4E / CHW4A: ego; LoRes4A: allo), NULL for the others; both NULL
+ * turns it off.  Each step's frame of a stacked view is written once, channel-planar, into slot w % K (and
+ * K + w % K when w % K < 3; w = the number of mg_step calls so far), a freshly reset env into the slots of
+ * frames w-3 .. w, instead of the [96][96][12] stack and its frame ring: the stack is the strided view of the
+ * ring at slot mg_window_start() with strides (env (K + 3) * 27648, y 96, x 1, channel 9216), value for value
+ * the stack mg_bind_outputs would receive (FlattenFrameStack / EagerDictFrameStack, benchmarks/__init__.py:
+ * 51-147).  The stacked outputs of mg_bind_outputs may then be NULL.  Bind before mg_reset; not with
+ * frames_only outputs.  A step's views stay valid until the next mg_step / mg_reset on the stream. */
+int mg_bind_window(mg_sim *sim, uint8_t *ring_allo, uint8_t *ring_ego, int32_t K);
+/* *slot = the window's first slot for the current outputs ((w + K - 3) % K), -1 when no ring is bound */
+int mg_window_start(const mg_sim *sim, int32_t *slot);
 void mg_destroy(mg_sim *sim);
 const char *mg_last_error(void);
 

@@ -26,6 +26,12 @@ struct RenderOut {
     int force_retry;      // tests: classes below this level hand every pair on (1: skip the first, 2: the first two)
     int scache_mode;      // tests / A-B (MG_DEBUG_SCACHE): 1 = no allocentric static layer, 2 = its copied blocks
                           // poisoned (0x55) -- shows where the layer is used
+    // window rings (mg_bind_window): a stacked view writes its current frame channel-planar into
+    // wring[view] u8[N][wK + 3][3][96][96] (slot wstep % wK, and wK + that slot when < 3; a fresh env the slots
+    // of frames wstep-3 .. wstep) instead of its [96][96][12] stack and frame ring; null: the stack as before
+    uint8_t *wring[2];
+    int wK;
+    long long wstep;
 };
 
 hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream_t st);

@@ -811,8 +811,13 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     // frames-only outputs (compact multi-GPU gather): the current frame of each view, no stacks, no ring
     // (the receivers rebuild the stacks: mg_restack)
     const bool fo = out.frames_only != 0;
-    const bool stacked = !fo && (pp == MG_PREPROC_LORESSTACK || (pp == MG_PREPROC_LORES4E && view == 1) ||
-                                 (pp == MG_PREPROC_LORES4A && view == 0));
+    const bool stacked0 = !fo && (pp == MG_PREPROC_LORESSTACK || (pp == MG_PREPROC_LORES4E && view == 1) ||
+                                  (pp == MG_PREPROC_LORES4A && view == 0));
+    // window ring (mg_bind_window): the stack of this view is a strided view of a ring the current frame is
+    // written into once, channel-planar (as mg_restack_window's rings) -- no [96][96][12] stack, no frame ring
+    uint8_t *const wring = (mode == 0 && stacked0) ? out.wring[view] : nullptr;
+    const bool win = wring != nullptr;
+    const bool stacked = stacked0 && !win;
     const bool plain = fo || pp != MG_PREPROC_LORESSTACK;   // the view's own current-frame output
     // frame ring kept only where a stack reads it (LoRes3EA: ego ring, read by compose3ea_kernel)
     const bool keep_ring = stacked || (!fo && pp == MG_PREPROC_LORES3EA && view == 1);
@@ -1168,11 +1173,42 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         for (int i = tid; i < ((dskip & 128) ? 0 : (int)(sizeof(sm.u.post.band) / 16)); i += RG_THREADS)
             ((uint4 *)&sm.u.post.band[0][0])[i] = make_uint4(0, 0, 0, 0);
         if (tid == 0) sm.nlong = 0;
+        const uint8_t *lo8c = (const uint8_t *)sm.u.post.lo;
         if (mode == 0 && !(dskip & 4)) {
             if (tid >= 64) {
                 // ring of the last 4 LoRes frames: slot nh (all 4 slots at episode start)
                 const int nring = keep_ring ? (fresh ? 4 : 1) * RG_BANDLO16 : 0;
                 const int nplain = nring + (plain ? RG_BANDLO16 : 0);
+                // window ring: the band's 2 LoRes rows per colour plane (2 x 96 B) into each slot of this step's
+                // frame (fresh: of frames t-3 .. t), 36 x 16 B per slot
+                const int wK = out.wK, wp = win ? (int)(out.wstep % wK) : 0;
+                int nsl = 0;
+                for (int d = 0; d < (fresh ? 4 : 1); d++) nsl += (wp + wK - d) % wK < 3 ? 2 : 1;
+                const int nwin = win ? nsl * RG_BANDLO16 : 0;
+                if (win) {
+                    for (int t = tid - 64; t < nwin; t += RG_THREADS - 64) {
+                        // the t / 36-th slot of the list: frames t, t-1, t-2, t-3 (fresh) each at f and, when
+                        // f < 3, at wK + f
+                        int k = t / RG_BANDLO16, slot = -1;
+                        for (int d = 0; d < (fresh ? 4 : 1) && slot < 0; d++) {
+                            const int f = (wp + wK - d) % wK;
+                            if (k == 0) slot = f;
+                            else if (f < 3 && k == 1) slot = wK + f;
+                            k -= f < 3 ? 2 : 1;
+                        }
+                        const int c = t % RG_BANDLO16, pl = c / 12, j = c % 12;   // plane, 16-byte chunk of it
+                        uint32_t w4[4];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            uint32_t v = 0u;
+#pragma unroll
+                            for (int b = 0; b < 4; b++) v |= (uint32_t)lo8c[(16 * j + 4 * q + b) * 3 + pl] << (8 * b);
+                            w4[q] = v;
+                        }
+                        *(uint4 *)(wring + ((size_t)e * (wK + 3) + slot) * FR + (size_t)pl * (MG_LORES * MG_LORES) +
+                                   (size_t)(y0 / 4) * MG_LORES + 16 * j) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                    }
+                }
                 for (int t = tid - 64; t < nplain + (mk_cache ? RG_BANDLO16 : 0); t += RG_THREADS - 64) {
                     if (t < nring) {
                         const int sl = fresh ? t / RG_BANDLO16 : nh, c = t % RG_BANDLO16;

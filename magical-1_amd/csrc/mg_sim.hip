@@ -57,6 +57,11 @@ struct mg_sim {
     int task, flags, preproc, max_steps, device, auto_reset;
     mg_buffers out;
     int bound;
+    // window rings of the stacked views (mg_bind_window; null: materialised stacks), their period, and the step
+    // counter that picks the slot (advanced by every mg_step before its render; resets do not advance it)
+    uint8_t *wring[2];
+    int wK;
+    long long wstep;
     StepCaps caps;     // the task's per-env slot caps
     int step_variant;  // compiled LDS-resident step variant (0: HBM state)
     int step_blk;      // envs per step workgroup
@@ -303,6 +308,7 @@ static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
     ro.obs_allo = s->out.obs_allo; ro.obs_ego = s->out.obs_ego; ro.obs_past = s->out.obs_past;
     ro.preproc = s->preproc;
     ro.frames_only = s->out.frames_only;
+    ro.wring[0] = s->wring[0]; ro.wring[1] = s->wring[1]; ro.wK = s->wK; ro.wstep = s->wstep;
     HIPC(mg_launch_render(s->S, s->dlib, ro, 0, st));
     if (s->preproc == MG_PREPROC_LORES3EA && !s->out.frames_only)
         HIPC(mg_launch_compose3ea(s->S, (const uint8_t *)s->out.obs_allo, mask, (uint8_t *)s->out.obs_past, st));
@@ -357,6 +363,7 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     mg_sim *s = new mg_sim();
     memset(&s->S, 0, sizeof(MGState));
     s->timing = 0; s->ev_used = 0; s->bound = 0;
+    s->wring[0] = s->wring[1] = nullptr; s->wK = 0; s->wstep = 0;
     s->task = cfg->task; s->flags = cfg->rand_flags; s->preproc = cfg->preproc;
     s->max_steps = cfg->max_episode_steps; s->device = cfg->device; s->auto_reset = cfg->auto_reset;
     s->S.n_envs = cfg->num_envs;
@@ -443,13 +450,17 @@ int mg_seed(mg_sim *s, const uint32_t *seeds_host) {
 
 int mg_bind_outputs(mg_sim *s, const mg_buffers *b) {
     if (!s || !b) return set_err(-22, "mg_bind_outputs: null argument");
-    if (s->preproc != MG_PREPROC_NONE && (!b->obs_allo || !b->obs_ego))
+    // with window rings bound (mg_bind_window) the stacked outputs are views of the rings: LoResStack's
+    // obs_allo / obs_ego and LoRes4E / LoRes4A's obs_past may be null
+    const bool win = !b->frames_only && (s->wring[0] || s->wring[1]);
+    const bool stack_ae = s->preproc == MG_PREPROC_LORESSTACK;
+    if (s->preproc != MG_PREPROC_NONE && (!b->obs_allo || !b->obs_ego) && !(win && stack_ae))
         return set_err(-22, "mg_bind_outputs: obs_allo / obs_ego required");
     if (b->frames_only != 0 && b->frames_only != 1) return set_err(-22, "mg_bind_outputs: frames_only must be 0 or 1");
     if (b->frames_only && s->preproc == MG_PREPROC_NONE)
         return set_err(-22, "mg_bind_outputs: frames_only needs a LoRes preprocessor");
     if ((s->preproc == MG_PREPROC_LORES4E || s->preproc == MG_PREPROC_LORES4A || s->preproc == MG_PREPROC_LORES3EA) &&
-        !b->frames_only && !b->obs_past)
+        !b->frames_only && !b->obs_past && !(win && s->preproc != MG_PREPROC_LORES3EA))
         return set_err(-22, "mg_bind_outputs: obs_past required for this preprocessor");
     const void *ptrs[3] = {b->obs_allo, b->obs_ego, b->frames_only ? nullptr : b->obs_past};
     for (const void *p : ptrs)
@@ -505,6 +516,7 @@ int mg_step(mg_sim *s, const uint8_t *actions, void *stream) {
     }
     if (ev) HIPC(hipEventRecord(ev[2], st));
     int rc = 0;
+    s->wstep++;   // this step's frame goes to the window rings' next slot
     if (s->preproc != MG_PREPROC_NONE) rc = render_lores(s, st, nullptr);
     if (ev) HIPC(hipEventRecord(ev[3], st));
     return rc;
@@ -584,6 +596,29 @@ int mg_restack_window(const uint8_t *recv, int32_t world, int32_t n, int64_t ran
         if (a & 15) return set_err(-22, "mg_restack_window: recv, ring, rank_stride and frame offsets must be 16-byte aligned");
     HIPC(mg_launch_restack_window(recv, world, n, rank_stride, off_allo, off_ego, off_done, preproc, step, all_fresh, K,
                                   ring, as_stream(stream)));
+    return 0;
+}
+
+int mg_bind_window(mg_sim *s, uint8_t *ring_allo, uint8_t *ring_ego, int32_t K) {
+    if (!s) return set_err(-22, "mg_bind_window: null sim");
+    if (!ring_allo && !ring_ego) { s->wring[0] = s->wring[1] = nullptr; s->wK = 0; return 0; }
+    if (K < 4 || K > 64) return set_err(-22, "mg_bind_window: K must be in [4, 64]");
+    const int pp = s->preproc;
+    const bool want_a = pp == MG_PREPROC_LORESSTACK || pp == MG_PREPROC_LORES4A;
+    const bool want_e = pp == MG_PREPROC_LORESSTACK || pp == MG_PREPROC_LORES4E;
+    if (!want_a && !want_e)
+        return set_err(-22, "mg_bind_window: preproc must be 1 (LoRes4E), 2 (LoResStack) or 4 (LoRes4A)");
+    if ((ring_allo != nullptr) != want_a || (ring_ego != nullptr) != want_e)
+        return set_err(-22, "mg_bind_window: a ring for each stacked view (LoResStack: allo and ego; LoRes4E: ego; "
+                            "LoRes4A: allo) and none for the others");
+    if (((uintptr_t)ring_allo | (uintptr_t)ring_ego) & 15) return set_err(-22, "mg_bind_window: rings must be 16-byte aligned");
+    s->wring[0] = ring_allo; s->wring[1] = ring_ego; s->wK = K;
+    return 0;
+}
+
+int mg_window_start(const mg_sim *s, int32_t *slot) {
+    if (!s || !slot) return set_err(-22, "mg_window_start: null argument");
+    *slot = s->wK > 0 ? (int32_t)((s->wstep + s->wK - 3) % s->wK) : -1;
     return 0;
 }
 

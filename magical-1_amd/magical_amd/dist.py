@@ -344,11 +344,13 @@ class ShardedVecEnv:
                                      "the chunks' resets wrote it")
                 from .pipeline import PipelinedVecEnv
                 vec = PipelinedVecEnv(env_name, envs_per_rank, chunks=chunks, device=dev_name, seeds=seeds,
-                                      max_episode_steps=max_episode_steps)
+                                      max_episode_steps=max_episode_steps, window=False)
             else:
                 from .envs import VecMagicalEnv
+                # the shard's outputs are bound into the packed buffers (frames: current frames only; stacked:
+                # materialised stacks), so no window rings on the simulator
                 vec = VecMagicalEnv(env_name, envs_per_rank, device=dev_name, seeds=seeds,
-                                    max_episode_steps=max_episode_steps)
+                                    max_episode_steps=max_episode_steps, window=False)
         self.vec = vec
         if gather:
             dev = torch.device(device) if device is not None else getattr(vec, "device", torch.device("cpu"))

@@ -10,7 +10,12 @@
 
 Every tensor VecMagicalEnv.reset()/step() returns (observations, reward, done,
 info values) is one of the simulator's bound output buffers: it is valid until
-the next reset()/step() rewrites it (clone it to keep it).
+the next reset()/step() rewrites it (clone it to keep it).  The frame stacks
+(LoRes4E / LoRes4A / CHW past_obs, LoResStack allo / ego) are by default strided
+views of per-view window rings on the device (mg_bind_window: each frame written
+once, channel-planar; the stack = 4 consecutive slots) -- the same values, shape
+and dtype as a contiguous stack, with channel stride 96 * 96 (permute(0, 3, 1, 2)
+gives contiguous NCHW per env); window=False materialises [N, 96, 96, 12] stacks.
 """
 import collections
 import ctypes
@@ -48,6 +53,23 @@ def _obs_shapes(spec):
 TARGET_KEYS = ("target_type", "target_colour", "target_position")
 
 
+WINDOW_K = 8   # window ring period: K + 3 slots per env and stacked view (magical_amd.dist uses the same)
+
+
+def window_views(spec):
+    """(allo, ego): which views of a preprocessor are frame stacks a window ring can hold (LoRes3EA's stack is
+    allo + 3 ego frames: not one ring's window)."""
+    pp = spec.preproc
+    return (pp in ("LoResStack", "LoRes4A"), pp in ("LoResStack", "LoRes4E", "LoResCHW4E", "LoResCHW4A"))
+
+
+def window_stack(ring, s0, K=WINDOW_K):
+    """[n, 96, 96, 12] stack view of a window ring u8[n, K + 3, 3, 96, 96] at first slot s0 (include/magical_sim.h
+    mg_bind_window): channel c = plane c % 3 of slot s0 + c // 3."""
+    fr = 96 * 96 * 3
+    return ring.as_strided((ring.shape[0], 96, 96, 12), ((K + 3) * fr, 96, 1, 96 * 96), ring.storage_offset() + s0 * fr)
+
+
 def observation_space(spec):
     items = [(k, spaces.Box(low=0, high=255, shape=s, dtype=np.uint8)) for k, s in _obs_shapes(spec).items()]
     if spec.task == "PickAndPlace":
@@ -62,7 +84,7 @@ class VecMagicalEnv:
     """Batched MAGICAL env on one MI355X (C ABI: include/magical_sim.h)."""
 
     def __init__(self, env_name, num_envs, device="cuda:0", seeds=None, base_seed=0, auto_reset=True,
-                 max_episode_steps=None, debug_reward=None):
+                 max_episode_steps=None, debug_reward=None, window=True):
         self.spec = registry.lookup(env_name)
         if not self.spec.gpu_supported:
             raise NotImplementedError(f"{env_name}: task not on the GPU hot path yet")
@@ -102,23 +124,31 @@ class VecMagicalEnv:
         self.handle = handle
         n, dev = self.num_envs, self.device
         u8 = dict(dtype=torch.uint8, device=dev)
+        wa, we = window_views(self.spec) if window and pp is not None else (False, False)
+        self.window_k = WINDOW_K if (wa or we) else 0
+        self.wring = [None, None]
+        if self.window_k:
+            shape = (n, self.window_k + 3, 3, 96, 96)
+            self.wring = [torch.zeros(shape, **u8) if wa else None, torch.zeros(shape, **u8) if we else None]
         if pp is None:
             self.full = torch.empty((n, 2, 384, 384, 3), **u8)
             self.obs_allo = self.obs_ego = self.obs_past = None
         elif pp == "LoResStack":
-            self.obs_allo = torch.empty((n, 96, 96, 12), **u8)
-            self.obs_ego = torch.empty((n, 96, 96, 12), **u8)
+            self.obs_allo = None if wa else torch.empty((n, 96, 96, 12), **u8)
+            self.obs_ego = None if we else torch.empty((n, 96, 96, 12), **u8)
             self.obs_past = None
         else:
             self.obs_allo = torch.empty((n, 96, 96, 3), **u8)
             self.obs_ego = torch.empty((n, 96, 96, 3), **u8)
-            self.obs_past = torch.empty((n, 96, 96, 12), **u8)
+            self.obs_past = None if self.window_k else torch.empty((n, 96, 96, 12), **u8)
         self.reward = torch.zeros(n, dtype=torch.float32, device=dev)
         self.done = torch.zeros(n, dtype=torch.bool, device=dev)  # the C ABI writes u8 0/1: same bytes
         self.eval_score = torch.zeros(n, dtype=torch.float64, device=dev)
         self.target = torch.zeros((n, 4), dtype=torch.float64, device=dev) if self.spec.task == "PickAndPlace" else None
         self.frames_only = False
         self.reset_count = 0   # explicit reset() calls (magical_amd.dist checks its frame rings against it)
+        if self.window_k:
+            self._bind_window()
         self._bind()
         self.action_space = spaces.Discrete(18)
         self.observation_space = observation_space(self.spec)
@@ -133,6 +163,24 @@ class VecMagicalEnv:
         buf.frames_only = 1 if self.frames_only else 0
         native.check(self.lib.mg_bind_outputs(self.handle, ctypes.byref(buf)))
 
+    def _bind_window(self):
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        native.check(self.lib.mg_bind_window(self.handle, ptr(self.wring[0]), ptr(self.wring[1]), self.window_k))
+
+    def bind_window(self, ring_allo, ring_ego):
+        """Use caller-owned window rings u8[n, K + 3, 3, 96, 96] (e.g. slices of a pool's rings: every env of a
+        magical_amd.pipeline pool in one ring) instead of this env's own; before the next reset()."""
+        if not self.window_k:
+            raise ValueError("bind_window: this env materialises its stacks (window=False or no stacked view)")
+        self.wring = [ring_allo if self.wring[0] is not None else None, ring_ego if self.wring[1] is not None else None]
+        self._bind_window()
+
+    def window_start(self):
+        """First slot of the current outputs' window (mg_window_start)."""
+        s0 = ctypes.c_int32()
+        native.check(self.lib.mg_window_start(self.handle, ctypes.byref(s0)))
+        return s0.value
+
     def bind_outputs(self, views, frames_only=False, target=None):
         """Write the following steps' outputs into caller-owned device tensors (e.g. views into one packed
         buffer per step, magical_amd.dist.PackedLayout): keys as output_buffers().  frames_only: 'allo' /
@@ -143,7 +191,7 @@ class VecMagicalEnv:
         f64 tensor to use instead -- bind it before the reset that fills it (magical_amd.pipeline)."""
         if self.spec.preproc is None:
             raise ValueError("bind_outputs: the unwrapped 384^2 view is rendered on demand, not bound")
-        self.obs_allo, self.obs_ego = views["allo"], views["ego"]
+        self.obs_allo, self.obs_ego = views.get("allo"), views.get("ego")   # (window-ring stacks: not bound)
         self.obs_past = None if frames_only else views.get("past_obs")
         self.reward, self.done, self.eval_score = views["reward"], views["done"], views["eval_score"]
         if self.target is not None and target is not None:
@@ -153,7 +201,7 @@ class VecMagicalEnv:
 
     def output_buffers(self):
         """The currently bound output tensors: raw (HWC) observation buffers, reward, done, eval_score[, target]."""
-        out = collections.OrderedDict([("allo", self.obs_allo), ("ego", self.obs_ego)])
+        out = collections.OrderedDict((k, v) for k, v in (("allo", self.obs_allo), ("ego", self.obs_ego)) if v is not None)
         if self.obs_past is not None:
             out["past_obs"] = self.obs_past
         out["reward"], out["done"], out["eval_score"] = self.reward, self.done, self.eval_score
@@ -167,15 +215,23 @@ class VecMagicalEnv:
     def _obs(self):
         if self.spec.preproc is None:
             out = collections.OrderedDict([("allo", self.full[:, 0]), ("ego", self.full[:, 1])])
+            past = None
         else:
-            out = collections.OrderedDict([("allo", self.obs_allo), ("ego", self.obs_ego)])
+            allo, ego, past = self.obs_allo, self.obs_ego, self.obs_past
+            if self.window_k and not self.frames_only:
+                s0 = self.window_start()
+                if self.spec.preproc == "LoResStack":
+                    allo, ego = window_stack(self.wring[0], s0, self.window_k), window_stack(self.wring[1], s0, self.window_k)
+                else:
+                    past = window_stack(self.wring[0] if self.wring[0] is not None else self.wring[1], s0, self.window_k)
+            out = collections.OrderedDict([("allo", allo), ("ego", ego)])
             if self._chw:
                 out = collections.OrderedDict((k, v.permute(0, 3, 1, 2)) for k, v in out.items())
         if self.target is not None:  # as SB3's DummyVecEnv buffers them: float32 per the spaces
             t = self.target.to(torch.float32)
             out["target_type"], out["target_colour"], out["target_position"] = t[:, 0:1], t[:, 1:2], t[:, 2:4]
-        if self.obs_past is not None:
-            out["past_obs"] = self.obs_past.permute(0, 3, 1, 2) if self._chw else self.obs_past
+        if past is not None:
+            out["past_obs"] = past.permute(0, 3, 1, 2) if self._chw else past
         return out
 
     # -- API -----------------------------------------------------------------

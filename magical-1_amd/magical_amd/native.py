@@ -14,8 +14,8 @@ if os.environ.get("MAGICAL_AMD_EXP_LIB"):   # A/B kernel experiments (tools/gpu_
 
 EXPORTS = ["mg_create", "mg_bind_outputs", "mg_reset", "mg_step", "mg_render_full", "mg_get_bodies",
            "mg_set_body_pose", "mg_get_errors", "mg_seed", "mg_random_actions", "mg_num_envs", "mg_enable_timing", "mg_read_timing",
-           "mg_set_episode_steps", "mg_selftest_sincos", "mg_replay_lores", "mg_restack", "mg_restack_window", "mg_destroy",
-           "mg_last_error"]
+           "mg_set_episode_steps", "mg_selftest_sincos", "mg_replay_lores", "mg_restack", "mg_restack_window", "mg_bind_window",
+           "mg_window_start", "mg_destroy", "mg_last_error"]
 
 
 class mg_config(ctypes.Structure):
@@ -72,6 +72,9 @@ def load():
     if hasattr(lib, "mg_restack_window"):
         i64 = ctypes.c_int64
         lib.mg_restack_window.argtypes = [vp, i32, i32, i64, i64, i64, i64, i32, i64, i32, i32, vp, vp]
+    if hasattr(lib, "mg_bind_window"):
+        lib.mg_bind_window.argtypes = [vp, vp, vp, i32]
+        lib.mg_window_start.argtypes = [vp, ctypes.POINTER(i32)]
     lib.mg_destroy.argtypes = [vp]
     lib.mg_destroy.restype = None
     lib.mg_last_error.restype = ctypes.c_char_p

@@ -65,8 +65,15 @@ class PipelinedVecEnv:
         self.buffers = collections.OrderedDict(
             (k, torch.zeros((num_envs,) + tuple(v.shape[1:]), dtype=v.dtype, device=self.device))
             for k, v in s0.output_buffers().items())
+        # window rings of the stacked views (VecMagicalEnv window mode): one ring per view for the whole pool,
+        # chunk k's envs a contiguous slice of it (env-major), so the pool's stacks are one strided view
+        self.window_k = s0.window_k
+        self.wring = [None if r is None else torch.zeros((num_envs,) + tuple(r.shape[1:]), dtype=r.dtype, device=self.device)
+                      for r in s0.wring]
         for k, sim in enumerate(self.sims):
             views = {key: buf[b[k]:b[k + 1]] for key, buf in self.buffers.items()}
+            if self.window_k:
+                sim.bind_window(*[None if r is None else r[b[k]:b[k + 1]] for r in self.wring])
             sim.bind_outputs(views, target=views.get("target"))
         # (a high-priority stream for chunk 0 measured no different, round 4: profiles/r04_resetwaves/)
         self.streams = [torch.cuda.Stream(self.device) for _ in range(chunks)]
@@ -145,15 +152,22 @@ class PipelinedVecEnv:
         return self._obs(), self.buffers["reward"], self.buffers["done"], {"eval_score": self.buffers["eval_score"]}
 
     def _obs(self):
-        out = collections.OrderedDict([("allo", self.buffers["allo"]), ("ego", self.buffers["ego"])])
+        from .envs import window_stack
+        allo, ego, past = self.buffers.get("allo"), self.buffers.get("ego"), self.buffers.get("past_obs")
+        if self.window_k:   # every chunk has stepped as often: one window start for the whole pool
+            s0, K = self.sims[0].window_start(), self.window_k
+            if self.spec.preproc == "LoResStack":
+                allo, ego = window_stack(self.wring[0], s0, K), window_stack(self.wring[1], s0, K)
+            else:
+                past = window_stack(self.wring[0] if self.wring[0] is not None else self.wring[1], s0, K)
+        out = collections.OrderedDict([("allo", allo), ("ego", ego)])
         if self.sims[0]._chw:
             out = collections.OrderedDict((k, v.permute(0, 3, 1, 2)) for k, v in out.items())
         if "target" in self.buffers:
             t = self.buffers["target"].to(torch.float32)
             out["target_type"], out["target_colour"], out["target_position"] = t[:, 0:1], t[:, 1:2], t[:, 2:4]
-        if "past_obs" in self.buffers:
-            p = self.buffers["past_obs"]
-            out["past_obs"] = p.permute(0, 3, 1, 2) if self.sims[0]._chw else p
+        if past is not None:
+            out["past_obs"] = past.permute(0, 3, 1, 2) if self.sims[0]._chw else past
         return out
 
     def random_actions(self, step, key=42, out=None):

@@ -399,6 +399,43 @@ def test_full_size_sampled_parity(name, n, steps, L):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name,n,L", [("MoveToRegion-Demo-LoRes4E-v0", 70, 9), ("MoveToRegion-Demo-LoRes4A-v0", 70, 9),
+                                      ("ClusterColour-Demo-LoResStack-v0", 66, 9),
+                                      ("MoveToCorner-Demo-LoResCHW4E-v0", 40, 7)])
+def test_window_stacks_match_materialised(name, n, L):
+    """The simulator's window rings (mg_bind_window, the make_vec default): every stacked output, read as the
+    strided view of its ring, equals the materialised stack of a window=False env (and so the oracle's: the
+    rollout tests run window mode) bit for bit over 30 steps -- the ring (K = 8) wraps three times, episodes of L
+    steps end in auto-resets that refill the window, and a masked explicit reset at step 15 refills some envs'
+    windows while the others keep theirs."""
+    seeds = [500 + i for i in range(n)]
+    a = magical_amd.make_vec(name, n, seeds=seeds, max_episode_steps=L)
+    b = magical_amd.make_vec(name, n, seeds=seeds, max_episode_steps=L, window=False)
+    assert a.window_k == 8 and b.window_k == 0
+    oa, ob = a.reset(), b.reset()
+    stacked = [k for k in oa if oa[k].shape[-1] == 12 or (oa[k].dim() == 4 and oa[k].shape[1] == 12)]
+    assert stacked and all(not oa[k].is_contiguous() for k in stacked)
+    acts = np.random.RandomState(8).randint(0, 18, (30, n))
+    mask = torch.from_numpy((np.random.RandomState(9).rand(n) < 0.3).astype(np.uint8)).cuda()
+    for t in range(30):
+        for k in ob:
+            assert torch.equal(oa[k], ob[k]), (t, k)
+        if t == 15:
+            oa, ob = a.reset(mask), b.reset(mask)
+            for k in ob:
+                assert torch.equal(oa[k], ob[k]), ("masked reset", k)
+        act = torch.as_tensor(acts[t], dtype=torch.uint8)
+        oa, ra, da, ia = a.step(act)
+        ob, rb, db, ib = b.step(act)
+        assert torch.equal(ra, rb) and torch.equal(da, db)
+    for k in ob:
+        assert torch.equal(oa[k], ob[k]), k
+    assert int(a.errors().abs().sum()) == 0
+    a.close()
+    b.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name,n,steps", [("MoveToRegion-Demo-LoRes4E-v0", 4096, 85),
                                           ("MoveToCorner-Demo-LoRes4E-v0", 4096, 165)])
 def test_full_size_pipelined_parity(name, n, steps):

@@ -57,9 +57,12 @@ if v[63]:
           f"{v[54]}, solid edges {v[55]}, bin entries {v[56]}; above caps: NV>768 {v[57]}, NV>896 {v[58]}, "
           f"bins>1536 {v[59]}, geoms>48 {v[60]}, dashes>128 {v[61]}, sedges>512 {v[62]}")
 tot = sum(v[32:42])
-waves = (n + 63) // 64
-print(f"physics: total {tot / 1e6:.1f}M ticks, {waves} waves")
+# one timer per workgroup (its first lane): the robot scenes' quad forms run blk envs per workgroup (16, or 8 below
+# 16 envs per CU), the cooperative form one env per workgroup
+robot = name.startswith(("MoveToRegion", "MoveToCorner"))
+blk = int(os.environ.get("MG_STEP_BLK", 0)) or ((16 if n >= 16 * 256 else 8) if robot else 1)
+wgs = (n + blk - 1) // blk
+print(f"physics: total {tot / 1e6:.1f}M ticks, {wgs} workgroups of {blk} envs")
 for i, nm in enumerate(P):
-    print(f"   {nm:32s} {v[32 + i] / max(tot, 1) * 100:6.1f}%  {v[32 + i] / (steps * waves):10.0f} per wave-step"
-          f"  {v[32 + i] / (steps * n):10.1f} per env-step (cooperative form: one env per wave)")
+    print(f"   {nm:32s} {v[32 + i] / max(tot, 1) * 100:6.1f}%  {v[32 + i] / (steps * wgs):10.0f} per workgroup-step")
 vec.close()

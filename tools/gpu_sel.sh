@@ -13,6 +13,6 @@ fi
 for ENV in "$@"; do
   N=4096; case $ENV in Cluster*|MatchRegions*) N=8192;; esac
   timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --env "$ENV" --envs $N > "$OUT/bench.$ENV.log" 2>&1
-  rc=$?; echo "bench $ENV rc=$rc"; tail -1 "$OUT/bench.$ENV.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['kernel_ms_per_step'])"; [ $rc -eq 0 ] || exit $rc
+  rc=$?; echo "bench $ENV rc=$rc"; tail -1 "$OUT/bench.$ENV.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['kernel_ms_per_step'], {k: d['kernels'][k]['ms'] for k in ('step_kernel', 'render_kernel')}, d['kernels']['timing'])"; [ $rc -eq 0 ] || exit $rc
 done
 exit 0
