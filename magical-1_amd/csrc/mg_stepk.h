@@ -64,6 +64,79 @@ __device__ __forceinline__ void carve_view(MGState &V, unsigned char *smem, cons
     V.arb_cap = c.na;
 }
 
+// rows [0, rows) of a [row][N] HBM array <-> [row][BLK] LDS array (lane's column); for the
+// cp / acon / ahash blocks the HBM row of LDS row (k, r) is k * hcap + r
+template <typename T>
+__device__ __forceinline__ void xfer(T *lds, T *hbm, int rows, int blk, int lane, int N, int e, bool to_lds,
+                                     int r0 = 0, int rs = 1, int groups = 1, int lcap = 0, int hcap = 0) {
+#pragma unroll 1
+    for (int g = 0; g < groups; g++)
+#pragma unroll 2
+        for (int r = r0; r < rows; r += rs) {
+            const uint32_t li = (uint32_t)(g * lcap + r) * blk + lane, hi = (uint32_t)(g * hcap + r) * N + e;
+            if (to_lds) lds[li] = hbm[hi]; else hbm[hi] = lds[li];
+        }
+}
+
+// The cooperative form's transfer (one env per wavefront: rows r0 = lane, step 64, so each array is at most one
+// row per lane) with runtime loops: the compile-time form below raised its VGPRs 248 -> 276 (one wavefront per SIMD
+// instead of two), round 5.  HBM <-> LDS view transfer of what the substeps read (in) / what later env-steps need (out):
+// bodies (incl. bias velocities and the rotation cache), the constraints' parameters and
+// warm-start impulses, the live arbiters (key, contacts, warm-start hashes) and the active list.
+// Cached shape BBs and the constraints' pre-step products are recomputed before use.
+// (r0, rs): rows r0, r0 + rs, ... of every array (rs = 64, r0 = lane: the cooperative form, one env per
+// wavefront, each lane a share of the rows)
+__device__ __forceinline__ void xfer_state(const MGState &S, const MGState &V, const StepCaps &c, int lane, int e,
+                                           bool in, bool cons_list = false, int r0 = 0, int rs = 1) {
+    const int blk = V.N, N = S.N;
+#define XF(f, rows) xfer(V.f, S.f, rows, blk, lane, N, e, in, r0, rs)
+#define XS(f, r) do { if (in) V.f[(uint32_t)(r) * blk + lane] = S.f[(uint32_t)(r) * N + e]; \
+                      else S.f[(uint32_t)(r) * N + e] = V.f[(uint32_t)(r) * blk + lane]; } while (0)
+    XF(bpx, c.nb); XF(bpy, c.nb); XF(bvx, c.nb); XF(bvy, c.nb); XF(ba, c.nb); XF(bw, c.nb); XF(bvbx, c.nb);
+    XF(bvby, c.nb); XF(bwb, c.nb); XF(brc, c.nb); XF(brs, c.nb); XF(bacache, c.nb);
+    // constraint parameter slots: in = MAXF, MAXB, BCOEF, JACC, JACC2, type parameters 8-11; out = JACC, JACC2
+#pragma unroll 1
+    for (int k = 0; k < CP_NUM; k++) {
+        const bool need = in ? (k <= CP_JACC2 || (k >= 8 && k <= 11)) : (k == CP_JACC || k == CP_JACC2);
+        if (!need) continue;
+#pragma unroll 2
+        for (int r = r0; r < c.nc; r += rs) {
+            const uint32_t li = (uint32_t)(k * c.nc + r) * blk + lane, hi = (uint32_t)(k * MG_MAX_CONS + r) * N + e;
+            if (in) V.cp[li] = S.cp[hi]; else S.cp[hi] = V.cp[li];
+        }
+    }
+#pragma unroll 1
+    for (int r = r0; r < c.na; r += rs) { // arbiter slots: only live ones carry data
+        XS(akey, r);
+        const int key = in ? V.akey[(uint32_t)r * blk + lane] : V.akey[(uint32_t)r * blk + lane];
+        if (key < 0) continue;
+        XS(anx, r); XS(any, r); XS(au, r); XS(astamp, r); XS(astate, r); XS(acount, r); XS(asa, r); XS(asb, r);
+#pragma unroll 1
+        for (int f = 0; f < 2 * AC_NUM; f++) {
+            if (in) V.acon[(uint32_t)(f * c.na + r) * blk + lane] = S.acon[(uint32_t)(f * MG_MAX_ARB + r) * N + e];
+            else S.acon[(uint32_t)(f * MG_MAX_ARB + r) * N + e] = V.acon[(uint32_t)(f * c.na + r) * blk + lane];
+        }
+        for (int k = 0; k < 2; k++) {
+            if (in) V.ahash[(uint32_t)(k * c.na + r) * blk + lane] = S.ahash[(uint32_t)(k * MG_MAX_ARB + r) * N + e];
+            else S.ahash[(uint32_t)(k * MG_MAX_ARB + r) * N + e] = V.ahash[(uint32_t)(k * c.na + r) * blk + lane];
+        }
+    }
+    XF(nactive, 1);
+    const int nact = in ? S.nactive[e] : V.nactive[lane];
+#pragma unroll 1
+    for (int r = r0; r < nact; r += rs) XS(active, r);
+    XF(curr_dt, 1); XF(stamp, 1); XF(overflow, 1);
+    if (in) { // read-only during the substeps
+        XF(target_speed, 1); XF(rel_turn, 1); XF(target_finger, 1);
+        XF(bminv, c.nb); XF(biinv, c.nb);
+        XF(sr, c.ns); XF(su, c.ns); XF(sgroup, c.ns); XF(shash, c.ns); XF(sbody, c.ns); XF(spoly, c.ns);
+        XF(nbodies, 1); XF(nshapes, 1); XF(ncons, 1); XF(robot_body0, 1); XF(robot_cons0, 1);
+        if (cons_list) { XF(ctype, c.nc); XF(ca, c.nc); XF(cb, c.nc); } // runtime constraint list
+    }
+#undef XS
+#undef XF
+}
+
 // HBM <-> LDS view transfer of what the substeps read (in) / what later env-steps need (out): bodies (incl. bias
 // velocities and the rotation cache), the constraints' parameters and warm-start impulses, the live arbiters
 // (key, contacts, warm-start hashes) and the active list; cached shape BBs and the constraints' pre-step products
@@ -88,17 +161,25 @@ MG_DEV void xq(T *lds, T *hbm, int blk, int lane, int N, int e, int sub, bool in
 template <int NB, int NS, int NC, int NA, int QL, bool CONS = false>
 __device__ __forceinline__ void xfer_state_quad(const MGState &S, const MGState &V, int lane, int e, int sub, bool in) {
     const int blk = V.N, N = S.N;
+    // groups of a few arrays are scheduled on their own (sched_barrier): their loads are in flight together,
+    // but the whole transfer is not hoisted into one block (that held ~200 VGPRs of loaded values and made
+    // the kernel spill)
 #define XQ(f, rows) xq<rows, QL>(V.f, S.f, blk, lane, N, e, sub, in)
-    XQ(bpx, NB); XQ(bpy, NB); XQ(bvx, NB); XQ(bvy, NB); XQ(ba, NB); XQ(bw, NB); XQ(bvbx, NB); XQ(bvby, NB);
-    XQ(bwb, NB); XQ(brc, NB); XQ(brs, NB); XQ(bacache, NB);
+#define XQ_GROUP() __builtin_amdgcn_sched_barrier(0)
+    XQ(bpx, NB); XQ(bpy, NB); XQ(bvx, NB); XQ(bvy, NB); XQ_GROUP();
+    XQ(ba, NB); XQ(bw, NB); XQ(bvbx, NB); XQ(bvby, NB); XQ_GROUP();
+    XQ(bwb, NB); XQ(brc, NB); XQ(brs, NB); XQ(bacache, NB); XQ_GROUP();
     if (in) {   // constraint parameter slots MAXF, MAXB, BCOEF, JACC, JACC2 and the type parameters 8-11
 #pragma unroll
-        for (int k = 0; k < CP_NUM; k++)
+        for (int k = 0; k < CP_NUM; k++) {
             if (k <= CP_JACC2 || (k >= 8 && k <= 11)) xq<NC, QL>(V.cp, S.cp, blk, lane, N, e, sub, true, k * NC, k * MG_MAX_CONS);
+            if (k == 2 || k == 8 || k == 11) XQ_GROUP();
+        }
     } else {    // the warm-start impulses
         xq<NC, QL>(V.cp, S.cp, blk, lane, N, e, sub, false, CP_JACC * NC, CP_JACC * MG_MAX_CONS);
         xq<NC, QL>(V.cp, S.cp, blk, lane, N, e, sub, false, CP_JACC2 * NC, CP_JACC2 * MG_MAX_CONS);
     }
+    XQ_GROUP();
     XQ(akey, NA);   // arbiter slots: only live ones carry data
 #pragma unroll
     for (int k = 0; k < (NA + QL - 1) / QL; k++) {
@@ -141,10 +222,12 @@ __device__ __forceinline__ void xfer_state_quad(const MGState &S, const MGState 
 #undef XS1
     }
     if (in) {   // read-only during the substeps
-        XQ(bminv, NB); XQ(biinv, NB);
-        XQ(sr, NS); XQ(su, NS); XQ(sgroup, NS); XQ(shash, NS); XQ(sbody, NS); XQ(spoly, NS);
+        XQ(bminv, NB); XQ(biinv, NB); XQ(sr, NS); XQ(su, NS); XQ_GROUP();
+        XQ(sgroup, NS); XQ(shash, NS); XQ(sbody, NS); XQ(spoly, NS);
         if constexpr (CONS) { XQ(ctype, NC); XQ(ca, NC); XQ(cb, NC); }
+        XQ_GROUP();
     }
+#undef XQ_GROUP
 #undef XQ
 }
 
@@ -251,10 +334,10 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
             __syncthreads();
             if (!own || sub != 0) return;
         } else {   // COOP
-            xfer_state_quad<C.nb, C.ns, C.nc, C.na, 64, true>(S, V, 0, e, lane, true);
+            xfer_state(S, V, C, 0, e, true, true, lane, 64);
             __syncthreads();
             env_substeps_coop(V, L, lane, a, P);
-            xfer_state_quad<C.nb, C.ns, C.nc, C.na, 64, true>(S, V, 0, e, lane, false);
+            xfer_state(S, V, C, 0, e, false, true, lane, 64);
             __syncthreads();
             if (lane != 0) return;
         }
