@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(64) step_kernel(MGState S, const mg_library *_
                 V.nbodies[lane] = 0; V.nshapes[lane] = 0; V.ncons[lane] = 0; V.nactive[lane] = 0;
             }
             env_substeps_quad<NCS, QL, (C.shw > 0)>(V, L, lane, sub, a, P);
-            if (own) xfer_state_quad<C.nb, C.ns, C.nc, C.na, QL>(S, V, lane, e, sub, false);
+            if (own) xfer_state(S, V, C, lane, e, false, false, sub, QL);   // stores: no latency chain to batch
             // the env's lane 0 scores from HBM rows its sibling lanes just wrote back: order them
             // by the memory model, not by one wavefront's in-order memory pipe
             __threadfence_block();

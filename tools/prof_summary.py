@@ -21,6 +21,28 @@ def kernel_stats(db):
     return [(short(r[0]), r[1], r[2], r[3], r[4]) for r in rows]
 
 
+def isolated_stats(db):
+    """Per kernel: calls and average duration (us) of the dispatches that overlap no other kernel dispatch in
+    time (bench.py's isolated pass: chunk 0 stepped alone), next to all dispatches."""
+    c = sqlite3.connect(db)
+    try:
+        rows = c.execute("select name, start, end from kernels order by start").fetchall()
+    except sqlite3.Error:
+        return {}
+    ev = [(short(n), s, e) for n, s, e in rows]
+    out = {}
+    max_end = -1
+    for i, (n, s, e) in enumerate(ev):
+        prev_overlap = max_end > s
+        nxt_overlap = i + 1 < len(ev) and ev[i + 1][1] < e
+        max_end = max(max_end, e)
+        d = out.setdefault(n, [0, 0.0, 0, 0.0])
+        d[0] += 1; d[1] += (e - s) / 1e3
+        if not prev_overlap and not nxt_overlap:
+            d[2] += 1; d[3] += (e - s) / 1e3
+    return {n: (d[0], d[1] / d[0], d[2], d[3] / d[2] if d[2] else None) for n, d in out.items()}
+
+
 def pmc(db):
     c = sqlite3.connect(db)
     q = ("select kernel_name, counter_name, count(*), avg(value), sum(value) from counters_collection "
@@ -36,6 +58,8 @@ def main():
     ap.add_argument("--kernel", default="render_kernel")
     ap.add_argument("--workload", default="MoveToRegion-Demo-LoRes4E-v0")
     ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--envs-per-launch", type=float, default=None,
+                    help="envs one launch of the kernel covers (chunked bench runs: envs / chunks)")
     a = ap.parse_args()
     out = []
     for db in sorted(glob.glob(os.path.join(a.dir, "**", "*.db"), recursive=True)):
@@ -52,6 +76,14 @@ def main():
             out.append(f"\n### kernel trace {sub}\n\n| kernel | calls | total us | avg us | % |\n|---|---|---|---|---|")
             for k, n, tot, avg, pct in kernel_stats(db):
                 out.append(f"| {k} | {n} | {tot:.0f} | {avg:.1f} | {pct:.2f} |")
+            iso = isolated_stats(db)
+            if iso:
+                out.append(f"\n#### isolated dispatches {sub} (overlapping no other kernel: bench.py's isolated pass)\n\n"
+                           "| kernel | isolated calls | isolated avg us | all calls | all avg us |\n|---|---|---|---|---|")
+                for k, (n, avg, ni, iavg) in sorted(iso.items(), key=lambda x: -x[1][0] * x[1][1]):
+                    if k.startswith(("at::", "__amd")) or n < 2:
+                        continue
+                    out.append(f"| {k} | {ni} | {iavg:.1f} | {n} | {avg:.1f} |" if iavg else f"| {k} | 0 | - | {n} | {avg:.1f} |")
     print("\n".join(out))
     if a.traffic_json:
         # FETCH_SIZE / WRITE_SIZE are KiB per dispatch; gfx950 FETCH_SIZE counts half of wide
@@ -76,6 +108,7 @@ def main():
         if fetch is not None and write is not None:
             data[a.kernel] = {"bytes_per_launch": round(fetch + write), "read_bytes": round(fetch),
                               "write_bytes": round(write), "source": a.dir, "workload": a.workload, "envs": a.envs,
+                              "envs_per_launch": a.envs_per_launch if a.envs_per_launch else a.envs,
                               "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->B"}
             if "SQ_INSTS_VALU" in sq and "GRBM_GUI_ACTIVE" in sq:
                 # VALU issue utilisation: a wave64 VALU instruction occupies a SIMD-32 for 2 cycles
