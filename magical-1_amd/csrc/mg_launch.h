@@ -27,11 +27,13 @@ struct RenderOut {
     int scache_mode;      // tests / A-B (MG_DEBUG_SCACHE): 1 = no allocentric static layer, 2 = its copied blocks
                           // poisoned (0x55) -- shows where the layer is used
     // window rings (mg_bind_window): a stacked view writes its current frame channel-planar into
-    // wring[view] u8[N][wK + 3][3][96][96] (slot wstep % wK, and wK + that slot when < 3; a fresh env the slots
-    // of frames wstep-3 .. wstep) instead of its [96][96][12] stack and frame ring; null: the stack as before
+    // wring[view] u8[N][wK + 3][3][96][96] (slot wpos = step % wK, and wK + wpos when wpos < 3; a fresh env the
+    // slots of frames step-3 .. step) instead of its [96][96][12] stack and frame ring; null: the stack as before
     uint8_t *wring[2];
-    int wK;
-    long long wstep;
+    int wK, wpos;
+    int wnsl[2];              // window slots of this step's frame: [0] a running env (wpos, and wK + wpos when
+    int8_t wsl[2][8];         // wpos < 3), [1] a fresh env (the slots of frames step-3 .. step, with duplicates)
+    int wdebug;               // experiments (MG_DEBUG_WIN): 1 = skip the window writes, 2 = write slot 0 only
 };
 
 hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream_t st);

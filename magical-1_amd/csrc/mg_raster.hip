@@ -6,8 +6,10 @@ hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderO
     const dim3 grid(S.n_envs, 2), blk(RG_THREADS);
     RenderOut r = ro;
     r.retry_in = r.retry_out = r.cls_level = 0;
+    if (mode == 0 && (ro.wring[0] || ro.wring[1]) && !ro.frames_only) mode = 2;   // window rings: own kernels
     if (ro.small) {   // the small class holds every MoveToRegion / MoveToCorner scene
         if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_SMALL>, 0>), grid, blk, 0, st, S, L, r);
+        else if (mode == 2) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_SMALL>, 2>), grid, blk, 0, st, S, L, r);
         else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_SMALL>, 1>), grid, blk, 0, st, S, L, r);
         return hipGetLastError();
     }
@@ -23,22 +25,26 @@ hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderO
     hipError_t e;
     if (r.first_level == 0) {
         if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM0>, 0>), grid, blk, 0, st, S, L, r);
+        else if (mode == 2) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM0>, 2>), grid, blk, 0, st, S, L, r);
         else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM0>, 1>), grid, blk, 0, st, S, L, r);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     r.cls_level = 1;
     if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM1>, 0>), grid, blk, 0, st, S, L, r);
+    else if (mode == 2) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM1>, 2>), grid, blk, 0, st, S, L, r);
     else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM1>, 1>), grid, blk, 0, st, S, L, r);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     r.cls_level = 2;
     if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM2>, 0>), grid, blk, 0, st, S, L, r);
+    else if (mode == 2) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM2>, 2>), grid, blk, 0, st, S, L, r);
     else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM2>, 1>), grid, blk, 0, st, S, L, r);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     r.retry_out = 0; r.cls_level = 3;
     if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_LARGE>, 0>), grid, blk, 0, st, S, L, r);
+    else if (mode == 2) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_LARGE>, 2>), grid, blk, 0, st, S, L, r);
     else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_LARGE>, 1>), grid, blk, 0, st, S, L, r);
     return hipGetLastError();
 }

@@ -469,7 +469,9 @@ MG_DEV void entity_xform(const MGState &S, int e, int ent, int x, double *xf) {
 template <class SM>
 MG_DEV int xf_slot(int ent, int x) { return x == MG_XF_MAIN ? ent : SM::RG_MAXE + x - 1; }
 
-// One (env, view) per workgroup.  mode 0: LoRes outputs; mode 1: full-resolution frames.
+// One (env, view) per workgroup.  MODE 0: LoRes outputs; 1: full-resolution frames; 2: LoRes outputs with the
+// stacked views as window rings (RenderOut::wring) -- its own instantiation, so the materialising kernels carry
+// none of its code (a shared build measured 4% slower render kernels, round 5).
 #ifndef RG_SMALL_WPE
 #define RG_SMALL_WPE 7                  // waves per SIMD the small class is compiled for: 72 VGPRs, 9 workgroups/CU
                                         // (measured: 7 -> 2.5% faster than the default 6; 8 = 64 VGPRs slower)
@@ -479,7 +481,8 @@ __global__ void __launch_bounds__(RG_THREADS)
 __attribute__((amdgpu_waves_per_eu((SM::RG_MAXG <= 32 && RG_SMALL_WPE) ? RG_SMALL_WPE : 1)))
 render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     __shared__ SM sm;
-    constexpr int mode = MODE;
+    constexpr int mode = MODE == 2 ? 0 : MODE;
+    constexpr bool WIN = MODE == 2;
     const int e = blockIdx.x, view = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
     if (e >= S.n_envs || (out.mask && !out.mask[e])) return;
     // class chain (many-block tasks): S.rg_retry[e][view] holds the chain level that holds this (env, view)
@@ -496,7 +499,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     // an episode's first allo frame invalidates the static layer of the previous episode before anything can
     // fail: a frame that a class hands over (or gives up on) must not leave the old layer marked valid
     // (ADVICE r3); a successful first frame of the layer's class sets it again at the end
-    if (MODE == 0 && view == 0 && tid == 0 && S.scache_ok && S.episode_steps[e] == 0) S.scache_ok[e] = 0;
+    if (mode == 0 && view == 0 && tid == 0 && S.scache_ok && S.episode_steps[e] == 0) S.scache_ok[e] = 0;
     MG_PROF_BEGIN(tid == 0);
     // capacity overflow: a class with a successor hands the (env, view) to it, else an env error
 #define RG_FAIL() do { \
@@ -815,8 +818,8 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                                   (pp == MG_PREPROC_LORES4A && view == 0));
     // window ring (mg_bind_window): the stack of this view is a strided view of a ring the current frame is
     // written into once, channel-planar (as mg_restack_window's rings) -- no [96][96][12] stack, no frame ring
-    uint8_t *const wring = (mode == 0 && stacked0) ? out.wring[view] : nullptr;
-    const bool win = wring != nullptr;
+    uint8_t *const wring = (WIN && stacked0) ? out.wring[view] : nullptr;
+    const bool win = WIN && wring != nullptr;
     const bool stacked = stacked0 && !win;
     const bool plain = fo || pp != MG_PREPROC_LORESSTACK;   // the view's own current-frame output
     // frame ring kept only where a stack reads it (LoRes3EA: ego ring, read by compose3ea_kernel)
@@ -833,7 +836,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     // The many-block tasks' classes are compiled without it: their scenes' blocks reach most bands, and
     // the layer's code measured slower there (ClusterColour 2.72 -> 3.00 ms, MatchRegions 3.37 -> 3.41 ms).
     constexpr bool kLayer = RG_SCACHE && SM::RG_MAXG <= 32;
-    const bool cview = kLayer && mode == 0 && view == 0 && out.scache_mode != 1 && !keep_ring && !stacked && plain;
+    const bool cview = kLayer && mode == 0 && view == 0 && out.scache_mode != 1 && !keep_ring && !stacked0 && plain;
     const bool mk_cache = cview && fresh && !SM::ORDMAX;
     const bool use_cache = cview && !fresh && S.scache_ok[e] != 0;
     uint8_t *const scache = S.scache + (size_t)e * FR;
@@ -1148,11 +1151,17 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                 }
             } else {
                 uint8_t *dst8 = sonly ? (uint8_t *)sm.u.post.los : lo8;
+                // window views: the same bytes channel-planar in `los` ([3][2 x 96]; a window view never uses the
+                // static layer that otherwise holds it), so the tail stores 16-byte chunks with no byte shuffle
+                uint8_t *pl8 = (WIN && win && !sonly) ? (uint8_t *)sm.u.post.los : nullptr;
                 for (int ch = 0; ch < ((dskip & 256) ? 0 : 3); ch++) {
                     const int ss = (int)((sum >> (16 * ch)) & 0xFFFF);
                     // round half to even of ss / 16: + 7, + 1 more when ss / 16 is odd
-                    if (RG_OFS) dst8[lpix * 3 + ch] = (uint8_t)((ss + 7 + ((ss >> 4) & 1)) >> 4);
-                    else { const int q = ss >> 4, rm = ss & 15; dst8[lpix * 3 + ch] = (uint8_t)(q + (rm > 8 || (rm == 8 && (q & 1)))); }
+                    uint8_t v8;
+                    if (RG_OFS) v8 = (uint8_t)((ss + 7 + ((ss >> 4) & 1)) >> 4);
+                    else { const int q = ss >> 4, rm = ss & 15; v8 = (uint8_t)(q + (rm > 8 || (rm == 8 && (q & 1)))); }
+                    dst8[lpix * 3 + ch] = v8;
+                    if (WIN && pl8) pl8[ch * (2 * MG_LORES) + lpix] = v8;
                 }
             }
         };
@@ -1173,42 +1182,11 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         for (int i = tid; i < ((dskip & 128) ? 0 : (int)(sizeof(sm.u.post.band) / 16)); i += RG_THREADS)
             ((uint4 *)&sm.u.post.band[0][0])[i] = make_uint4(0, 0, 0, 0);
         if (tid == 0) sm.nlong = 0;
-        const uint8_t *lo8c = (const uint8_t *)sm.u.post.lo;
         if (mode == 0 && !(dskip & 4)) {
             if (tid >= 64) {
                 // ring of the last 4 LoRes frames: slot nh (all 4 slots at episode start)
                 const int nring = keep_ring ? (fresh ? 4 : 1) * RG_BANDLO16 : 0;
                 const int nplain = nring + (plain ? RG_BANDLO16 : 0);
-                // window ring: the band's 2 LoRes rows per colour plane (2 x 96 B) into each slot of this step's
-                // frame (fresh: of frames t-3 .. t), 36 x 16 B per slot
-                const int wK = out.wK, wp = win ? (int)(out.wstep % wK) : 0;
-                int nsl = 0;
-                for (int d = 0; d < (fresh ? 4 : 1); d++) nsl += (wp + wK - d) % wK < 3 ? 2 : 1;
-                const int nwin = win ? nsl * RG_BANDLO16 : 0;
-                if (win) {
-                    for (int t = tid - 64; t < nwin; t += RG_THREADS - 64) {
-                        // the t / 36-th slot of the list: frames t, t-1, t-2, t-3 (fresh) each at f and, when
-                        // f < 3, at wK + f
-                        int k = t / RG_BANDLO16, slot = -1;
-                        for (int d = 0; d < (fresh ? 4 : 1) && slot < 0; d++) {
-                            const int f = (wp + wK - d) % wK;
-                            if (k == 0) slot = f;
-                            else if (f < 3 && k == 1) slot = wK + f;
-                            k -= f < 3 ? 2 : 1;
-                        }
-                        const int c = t % RG_BANDLO16, pl = c / 12, j = c % 12;   // plane, 16-byte chunk of it
-                        uint32_t w4[4];
-#pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            uint32_t v = 0u;
-#pragma unroll
-                            for (int b = 0; b < 4; b++) v |= (uint32_t)lo8c[(16 * j + 4 * q + b) * 3 + pl] << (8 * b);
-                            w4[q] = v;
-                        }
-                        *(uint4 *)(wring + ((size_t)e * (wK + 3) + slot) * FR + (size_t)pl * (MG_LORES * MG_LORES) +
-                                   (size_t)(y0 / 4) * MG_LORES + 16 * j) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-                    }
-                }
                 for (int t = tid - 64; t < nplain + (mk_cache ? RG_BANDLO16 : 0); t += RG_THREADS - 64) {
                     if (t < nring) {
                         const int sl = fresh ? t / RG_BANDLO16 : nh, c = t % RG_BANDLO16;
@@ -1220,6 +1198,17 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                         const int c = t - nplain;
                         *(uint4 *)(scache + lrow + 16 * c) = sm.u.post.los[c];
                     }
+                }
+            } else if (win) {
+                // window ring: the band's 2 LoRes rows of each colour plane (2 x 96 B, planar in `los` since the
+                // resolve) into every slot of this step's frame (fresh: of frames t-3 .. t; the slot lists come
+                // from the host, RenderOut::wsl), by wave 0 (the stack's wave): 36 x 16 B per slot
+                const int lst = fresh ? 1 : 0, nwin = out.wdebug == 1 ? 0 : out.wnsl[lst] * RG_BANDLO16;
+                for (int t = tid; t < nwin; t += 64) {
+                    const int slot = out.wdebug == 2 ? 0 : out.wsl[lst][t / RG_BANDLO16];
+                    const int c = t % RG_BANDLO16, pl = c / 12, j = c % 12;   // plane, 16-byte chunk of its 192 B
+                    *(uint4 *)(wring + ((size_t)e * (out.wK + 3) + slot) * FR + (size_t)pl * (MG_LORES * MG_LORES) +
+                               (size_t)(y0 / 4) * MG_LORES + 16 * j) = sm.u.post.los[c];
                 }
             } else if (stacked && tid < 2 * MG_LORES / 4 && !(dskip & 64)) {
                 // FlattenFrameStack: [96][96][12] = frames oldest..newest concatenated per pixel; one thread

@@ -308,7 +308,18 @@ static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
     ro.obs_allo = s->out.obs_allo; ro.obs_ego = s->out.obs_ego; ro.obs_past = s->out.obs_past;
     ro.preproc = s->preproc;
     ro.frames_only = s->out.frames_only;
-    ro.wring[0] = s->wring[0]; ro.wring[1] = s->wring[1]; ro.wK = s->wK; ro.wstep = s->wstep;
+    ro.wring[0] = s->wring[0]; ro.wring[1] = s->wring[1]; ro.wK = s->wK;
+    ro.wpos = s->wK > 0 ? (int)(s->wstep % s->wK) : 0;
+    for (int fr = 0; fr < 2 && s->wK > 0; fr++) {   // slot lists of a running / a fresh env (mg_bind_window)
+        int n = 0;
+        for (int d = 0; d < (fr ? 4 : 1); d++) {
+            const int f = (ro.wpos + s->wK - d) % s->wK;
+            ro.wsl[fr][n++] = (int8_t)f;
+            if (f < 3) ro.wsl[fr][n++] = (int8_t)(s->wK + f);
+        }
+        ro.wnsl[fr] = n;
+    }
+    ro.wdebug = getenv("MG_DEBUG_WIN") ? atoi(getenv("MG_DEBUG_WIN")) : 0;
     HIPC(mg_launch_render(s->S, s->dlib, ro, 0, st));
     if (s->preproc == MG_PREPROC_LORES3EA && !s->out.frames_only)
         HIPC(mg_launch_compose3ea(s->S, (const uint8_t *)s->out.obs_allo, mask, (uint8_t *)s->out.obs_past, st));

@@ -1100,75 +1100,21 @@ MG_DEV void xarb_row(LaneBodies &R, RobotV &V, int rb0, int lane, const MGState 
     else if (lane == 0) S.overflow[e] |= 32;
 #undef XROW
 }
-// The robot rows' pre-stepped terms, lane-distributed (round 5): they are constant over the 10 iterations, so
-// each lane t < RT_TERMS loads term t of the robot's ten joints once per substep (the joint's MAXF already
-// multiplied by dt: the same product the row forms each time) and the rows read them with readlane -- a VALU
-// op with no memory dependency, where the rows' LDS reads waited behind the arbiter rows' LDS stores (the
-// compiler cannot prove S.cp and S.acon apart) and behind one another (the 248-VGPR budget of two wavefronts
-// per SIMD leaves no room to hold them).  Terms per joint type, in this order:
-//   pivot R1X R1Y R2X R2Y BIAS BIAS2 K11 K12 K21 K22 JMAX; gear RATIO BIAS ISUM RATIO_INV JMAX;
-//   spring WCOEF ISUM; rotary limit BIAS ISUM JMAX; motor RATE ISUM JMAX.
-enum { RT_JMAX = -1 };
-__host__ __device__ constexpr int rt_count(int type) {
-    return type == MG_C_PIVOT ? 11 : type == MG_C_GEAR ? 5 : type == MG_C_SPRING ? 2 : 3;
-}
-__host__ __device__ constexpr int rt_field(int type, int i) {
-    if (type == MG_C_PIVOT) {
-        constexpr int F[11] = {CP_R1X, CP_R1Y, CP_R2X, CP_R2Y, CP_BIAS, CP_BIAS2, CP_K11, CP_K12, CP_K21, CP_K22, RT_JMAX};
-        return F[i];
-    }
-    if (type == MG_C_GEAR) { constexpr int F[5] = {CP_RATIO, CP_BIAS, CP_ISUM, CP_RATIO_INV, RT_JMAX}; return F[i]; }
-    if (type == MG_C_SPRING) { constexpr int F[2] = {CP_WCOEF, CP_ISUM}; return F[i]; }
-    if (type == MG_C_ROTLIMIT) { constexpr int F[3] = {CP_BIAS, CP_ISUM, RT_JMAX}; return F[i]; }
-    constexpr int F[3] = {CP_RATE, CP_ISUM, RT_JMAX};   // motor
-    return F[i];
-}
-__host__ __device__ constexpr int rt_base(int K) {
-    int b = 0;
-    for (int k = 0; k < K; k++) b += rt_count(static_cons(k).type);
-    return b;
-}
-constexpr int RT_TERMS = rt_base(10);
-static_assert(RT_TERMS <= 64, "one robot-row term per lane");
-// the lane of term `field` of joint K
+// robot joint K (static_cons(K): compile-time type and body slots) at list index c: lcons_cached /
+// lcons_apply with the bodies and accumulators in registers and the pre-stepped terms read from LDS
 template <int K>
-__host__ __device__ constexpr int rt_lane(int field) {
-    constexpr int type = static_cons(K).type;
-    for (int i = 0; i < rt_count(type); i++)
-        if (rt_field(type, i) == field) return rt_base(K) + i;
-    return -1;
-}
-// lane t's term (t < RT_TERMS; 0.0 elsewhere)
-MG_DEV double rt_load(const MGState &S, int e, int rc0, int t, double dt) {
-    double v = 0.0;
-#pragma unroll
-    for (int K = 0; K < 10; K++) {
-        const int type = static_cons(K).type, b = rt_base(K);
-#pragma unroll
-        for (int i = 0; i < rt_count(type); i++) {
-            const int f = rt_field(type, i);
-            if (t == b + i) v = f == RT_JMAX ? CPA(CP_MAXF, rc0 + K) * dt : CPA(f, rc0 + K);
-        }
-    }
-    return v;
-}
-#define RT(f) rl_d(tv, rt_lane<K>(f))
-
-// robot joint K (static_cons(K): compile-time type and body slots): lcons_cached / lcons_apply with the bodies
-// and accumulators in registers and the pre-stepped terms read from the lanes (tv, rt_load)
-template <int K>
-MG_DEV void rrow_apply(RobotV &V, double tv) {
+MG_DEV void rrow_apply(RobotV &V, const MGState &S, int e, int c, double dt) {
     constexpr ConsDesc d = static_cons(K);
     constexpr int a = d.a, b = d.b;
     if constexpr (d.type == MG_C_PIVOT) {
-        V2 r1 = v2(RT(CP_R1X), RT(CP_R1Y)), r2 = v2(RT(CP_R2X), RT(CP_R2Y));
+        V2 r1 = v2(CPA(CP_R1X, c), CPA(CP_R1Y, c)), r2 = v2(CPA(CP_R2X, c), CPA(CP_R2Y, c));
         V2 v1 = vadd(v2(V.vx[a], V.vy[a]), vmult(vperp(r1), V.w[a]));
         V2 v2_ = vadd(v2(V.vx[b], V.vy[b]), vmult(vperp(r2), V.w[b]));
         V2 vr = vsub(v2_, v1);
-        V2 dd = vsub(v2(RT(CP_BIAS), RT(CP_BIAS2)), vr);
-        V2 j = v2(dd.x * RT(CP_K11) + dd.y * RT(CP_K12), dd.x * RT(CP_K21) + dd.y * RT(CP_K22));
+        V2 dd = vsub(v2(CPA(CP_BIAS, c), CPA(CP_BIAS2, c)), vr);
+        V2 j = v2(dd.x * CPA(CP_K11, c) + dd.y * CPA(CP_K12, c), dd.x * CPA(CP_K21, c) + dd.y * CPA(CP_K22, c));
         V2 jOld = v2(V.jacc[K], V.jacc2[K]);
-        V2 jAcc = vclamp(vadd(jOld, j), RT(RT_JMAX));
+        V2 jAcc = vclamp(vadd(jOld, j), CPA(CP_MAXF, c) * dt);
         V.jacc[K] = jAcc.x; V.jacc2[K] = jAcc.y;
         V2 dj = vsub(jAcc, jOld);
         const V2 ja = vneg(dj);
@@ -1177,22 +1123,22 @@ MG_DEV void rrow_apply(RobotV &V, double tv) {
         V.vx[b] = V.vx[b] + dj.x * V.minv[b]; V.vy[b] = V.vy[b] + dj.y * V.minv[b];
         V.w[b] = V.w[b] + V.iinv[b] * vcross(r2, dj);
     } else if constexpr (d.type == MG_C_GEAR) {
-        double ratio = RT(CP_RATIO);
+        double ratio = CPA(CP_RATIO, c);
         double wr = V.w[b] * ratio - V.w[a];
-        double jMax = RT(RT_JMAX);
-        double j = (RT(CP_BIAS) - wr) * RT(CP_ISUM);
+        double jMax = CPA(CP_MAXF, c) * dt;
+        double j = (CPA(CP_BIAS, c) - wr) * CPA(CP_ISUM, c);
         double jOld = V.jacc[K];
         double jAcc = cpclamp(jOld + j, -jMax, jMax);
         V.jacc[K] = jAcc;
         j = jAcc - jOld;
-        V.w[a] = V.w[a] - j * V.iinv[a] * RT(CP_RATIO_INV);
+        V.w[a] = V.w[a] - j * V.iinv[a] * CPA(CP_RATIO_INV, c);
         V.w[b] = V.w[b] + j * V.iinv[b];
     } else if constexpr (d.type == MG_C_ROTLIMIT) {
-        double bias = RT(CP_BIAS);
+        double bias = CPA(CP_BIAS, c);
         if (!bias) return;
         double wr = V.w[b] - V.w[a];
-        double jMax = RT(RT_JMAX);
-        double j = -(bias + wr) * RT(CP_ISUM);
+        double jMax = CPA(CP_MAXF, c) * dt;
+        double j = -(bias + wr) * CPA(CP_ISUM, c);
         double jOld = V.jacc[K];
         double jAcc = bias < 0.0 ? cpclamp(jOld + j, 0.0, jMax) : cpclamp(jOld + j, -jMax, 0.0);
         V.jacc[K] = jAcc;
@@ -1200,9 +1146,9 @@ MG_DEV void rrow_apply(RobotV &V, double tv) {
         V.w[a] = V.w[a] - j * V.iinv[a];
         V.w[b] = V.w[b] + j * V.iinv[b];
     } else if constexpr (d.type == MG_C_MOTOR) {
-        double wr = V.w[b] - V.w[a] + RT(CP_RATE);
-        double jMax = RT(RT_JMAX);
-        double j = -wr * RT(CP_ISUM);
+        double wr = V.w[b] - V.w[a] + CPA(CP_RATE, c);
+        double jMax = CPA(CP_MAXF, c) * dt;
+        double j = -wr * CPA(CP_ISUM, c);
         double jOld = V.jacc[K];
         double jAcc = cpclamp(jOld + j, -jMax, jMax);
         V.jacc[K] = jAcc;
@@ -1211,21 +1157,21 @@ MG_DEV void rrow_apply(RobotV &V, double tv) {
         V.w[b] = V.w[b] + j * V.iinv[b];
     } else if constexpr (d.type == MG_C_SPRING) {
         double wrn = V.w[a] - V.w[b];
-        double w_damp = (V.twrn[K] - wrn) * RT(CP_WCOEF);
+        double w_damp = (V.twrn[K] - wrn) * CPA(CP_WCOEF, c);
         V.twrn[K] = wrn + w_damp;
-        double j_damp = w_damp * RT(CP_ISUM);
+        double j_damp = w_damp * CPA(CP_ISUM, c);
         V.jacc[K] = V.jacc[K] + j_damp;
         V.w[a] = V.w[a] + j_damp * V.iinv[a];
         V.w[b] = V.w[b] - j_damp * V.iinv[b];
     }
 }
 template <int K>
-MG_DEV void rrow_cached(RobotV &V, double tv, double dt_coef) {
+MG_DEV void rrow_cached(RobotV &V, const MGState &S, int e, int c, double dt_coef) {
     constexpr ConsDesc d = static_cons(K);
     constexpr int a = d.a, b = d.b;
     if constexpr (d.type == MG_C_PIVOT) {
         V2 j = vmult(v2(V.jacc[K], V.jacc2[K]), dt_coef);
-        const V2 r1 = v2(RT(CP_R1X), RT(CP_R1Y)), r2 = v2(RT(CP_R2X), RT(CP_R2Y));
+        const V2 r1 = v2(CPA(CP_R1X, c), CPA(CP_R1Y, c)), r2 = v2(CPA(CP_R2X, c), CPA(CP_R2Y, c));
         const V2 ja = vneg(j);
         V.vx[a] = V.vx[a] + ja.x * V.minv[a]; V.vy[a] = V.vy[a] + ja.y * V.minv[a];
         V.w[a] = V.w[a] + V.iinv[a] * vcross(r1, ja);
@@ -1233,7 +1179,7 @@ MG_DEV void rrow_cached(RobotV &V, double tv, double dt_coef) {
         V.w[b] = V.w[b] + V.iinv[b] * vcross(r2, j);
     } else if constexpr (d.type == MG_C_GEAR) {
         double j = V.jacc[K] * dt_coef;
-        V.w[a] = V.w[a] - j * V.iinv[a] * RT(CP_RATIO_INV);
+        V.w[a] = V.w[a] - j * V.iinv[a] * CPA(CP_RATIO_INV, c);
         V.w[b] = V.w[b] + j * V.iinv[b];
     } else if constexpr (d.type == MG_C_ROTLIMIT || d.type == MG_C_MOTOR) {
         double j = V.jacc[K] * dt_coef;
@@ -1241,14 +1187,13 @@ MG_DEV void rrow_cached(RobotV &V, double tv, double dt_coef) {
         V.w[b] = V.w[b] + j * V.iinv[b];
     }
 }
-#undef RT
 template <int K = 0>
-MG_DEV void rrows_cached(RobotV &V, double tv, double dt_coef) {
-    if constexpr (K < 10) { rrow_cached<K>(V, tv, dt_coef); rrows_cached<K + 1>(V, tv, dt_coef); }
+MG_DEV void rrows_cached(RobotV &V, const MGState &S, int e, int rc0, double dt_coef) {
+    if constexpr (K < 10) { rrow_cached<K>(V, S, e, rc0 + K, dt_coef); rrows_cached<K + 1>(V, S, e, rc0, dt_coef); }
 }
 template <int K = 0>
-MG_DEV void rrows_apply(RobotV &V, double tv) {
-    if constexpr (K < 10) { rrow_apply<K>(V, tv); rrows_apply<K + 1>(V, tv); }
+MG_DEV void rrows_apply(RobotV &V, const MGState &S, int e, int rc0, double dt) {
+    if constexpr (K < 10) { rrow_apply<K>(V, S, e, rc0 + K, dt); rrows_apply<K + 1>(V, S, e, rc0, dt); }
 }
 
 // the env's constraint list is the blocks' ground rows (G) plus the robot's ten joints at rc0 in
@@ -1436,9 +1381,7 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
             lground_cached(R, S, e, G.c0, dt_coef);
             if (G.n > 1) lground_cached(R, S, e, G.c1, dt_coef);
         }
-        // the robot rows' pre-stepped terms, one per lane (rt_load)
-        const double tv = lane < RT_TERMS ? rt_load(S, e, rc0, lane, dt) : 0.0;
-        rrows_cached(V, tv, dt_coef);
+        rrows_cached(V, S, e, rc0, dt_coef);
         MG_PP(P, 5);
 #pragma unroll 1
         for (int it = 0; it < MG_EXP_COOP_ITERS; it++) {
@@ -1452,7 +1395,7 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
             }
 #endif
 #ifndef MG_EXP_COOP_NOCONS
-            rrows_apply(V, tv);
+            rrows_apply(V, S, e, rc0, dt);
 #endif
         }
         // robot lanes: velocities from V (their bias velocities stayed in the lanes)
