@@ -263,9 +263,9 @@ def main():
     ap.add_argument("--iso-steps", type=int, default=20,
                     help="chunked runs: steps of chunk 0 alone after the timed region, for the roofline's isolated "
                          "per-kernel times (0: none)")
-    ap.add_argument("--stacks", default="window", choices=("window", "materialize"),
-                    help="the simulator's frame stacks: strided views of window rings (mg_bind_window, default) or "
-                         "materialised [N, 96, 96, 12] tensors")
+    ap.add_argument("--stacks", default="materialize", choices=("window", "materialize"),
+                    help="the simulator's frame stacks: materialised [N, 96, 96, 12] tensors (default) or strided "
+                         "views of window rings (mg_bind_window; measured slower in the render kernel)")
     ap.add_argument("--restack", default="window", choices=("window", "materialize"),
                     help="frames-mode receivers: window ring views (mg_restack_window) or materialised stacks "
                          "(mg_restack)")

@@ -33,7 +33,6 @@ struct RenderOut {
     int wK, wpos;
     int wnsl[2];              // window slots of this step's frame: [0] a running env (wpos, and wK + wpos when
     int8_t wsl[2][8];         // wpos < 3), [1] a fresh env (the slots of frames step-3 .. step, with duplicates)
-    int wdebug;               // experiments (MG_DEBUG_WIN): 1 = skip the window writes, 2 = write slot 0 only
 };
 
 hipError_t mg_launch_seed(const MGState &S, const uint32_t *seeds_dev, hipStream_t st);

@@ -1203,9 +1203,9 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                 // window ring: the band's 2 LoRes rows of each colour plane (2 x 96 B, planar in `los` since the
                 // resolve) into every slot of this step's frame (fresh: of frames t-3 .. t; the slot lists come
                 // from the host, RenderOut::wsl), by wave 0 (the stack's wave): 36 x 16 B per slot
-                const int lst = fresh ? 1 : 0, nwin = out.wdebug == 1 ? 0 : out.wnsl[lst] * RG_BANDLO16;
+                const int lst = fresh ? 1 : 0, nwin = out.wnsl[lst] * RG_BANDLO16;
                 for (int t = tid; t < nwin; t += 64) {
-                    const int slot = out.wdebug == 2 ? 0 : out.wsl[lst][t / RG_BANDLO16];
+                    const int slot = out.wsl[lst][t / RG_BANDLO16];
                     const int c = t % RG_BANDLO16, pl = c / 12, j = c % 12;   // plane, 16-byte chunk of its 192 B
                     *(uint4 *)(wring + ((size_t)e * (out.wK + 3) + slot) * FR + (size_t)pl * (MG_LORES * MG_LORES) +
                                (size_t)(y0 / 4) * MG_LORES + 16 * j) = sm.u.post.los[c];

@@ -319,7 +319,6 @@ static int render_lores(mg_sim *s, hipStream_t st, const uint8_t *mask) {
         }
         ro.wnsl[fr] = n;
     }
-    ro.wdebug = getenv("MG_DEBUG_WIN") ? atoi(getenv("MG_DEBUG_WIN")) : 0;
     HIPC(mg_launch_render(s->S, s->dlib, ro, 0, st));
     if (s->preproc == MG_PREPROC_LORES3EA && !s->out.frames_only)
         HIPC(mg_launch_compose3ea(s->S, (const uint8_t *)s->out.obs_allo, mask, (uint8_t *)s->out.obs_past, st));

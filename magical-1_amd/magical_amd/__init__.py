@@ -25,10 +25,10 @@ def make(env_name, device="cuda:0", seed=None, debug_reward=None):
 
 
 def make_vec(env_name, num_envs, device="cuda:0", seeds=None, base_seed=0, auto_reset=True, max_episode_steps=None,
-             debug_reward=None, window=True):
+             debug_reward=None, window=False):
     """num_envs instances of env_name on one GPU (batched, auto-resetting).  max_episode_steps
     overrides the registered episode length (gym.make(..., max_episode_steps=...)).  window: frame stacks as
-    strided views of window rings (default) or materialised [N, 96, 96, 12] tensors (False)."""
+    strided views of window rings (True) or materialised [N, 96, 96, 12] tensors (False, the default)."""
     from .envs import VecMagicalEnv
     return VecMagicalEnv(env_name, num_envs, device=device, seeds=seeds, base_seed=base_seed, auto_reset=auto_reset,
                          max_episode_steps=max_episode_steps, debug_reward=debug_reward, window=window)

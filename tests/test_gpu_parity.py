@@ -403,14 +403,14 @@ def test_full_size_sampled_parity(name, n, steps, L):
                                       ("ClusterColour-Demo-LoResStack-v0", 66, 9),
                                       ("MoveToCorner-Demo-LoResCHW4E-v0", 40, 7)])
 def test_window_stacks_match_materialised(name, n, L):
-    """The simulator's window rings (mg_bind_window, the make_vec default): every stacked output, read as the
-    strided view of its ring, equals the materialised stack of a window=False env (and so the oracle's: the
-    rollout tests run window mode) bit for bit over 30 steps -- the ring (K = 8) wraps three times, episodes of L
+    """The simulator's window rings (mg_bind_window, make_vec(window=True)): every stacked output, read as the
+    strided view of its ring, equals the materialised stack of the default env (and so the oracle's) bit for
+    bit over 30 steps -- the ring (K = 8) wraps three times, episodes of L
     steps end in auto-resets that refill the window, and a masked explicit reset at step 15 refills some envs'
     windows while the others keep theirs."""
     seeds = [500 + i for i in range(n)]
-    a = magical_amd.make_vec(name, n, seeds=seeds, max_episode_steps=L)
-    b = magical_amd.make_vec(name, n, seeds=seeds, max_episode_steps=L, window=False)
+    a = magical_amd.make_vec(name, n, seeds=seeds, max_episode_steps=L, window=True)
+    b = magical_amd.make_vec(name, n, seeds=seeds, max_episode_steps=L)
     assert a.window_k == 8 and b.window_k == 0
     oa, ob = a.reset(), b.reset()
     stacked = [k for k in oa if oa[k].shape[-1] == 12 or (oa[k].dim() == 4 and oa[k].shape[1] == 12)]
