@@ -175,6 +175,7 @@ MG_DEV void space_step_quad(const MGState &S, const mg_library *L, int e, int su
     const uint32_t stamp = S.stamp[e] + 1;
     const int nact0 = S.nactive[e], nb = S.nbodies[e], ns = S.nshapes[e];
     for (int i = sub; i < nact0; i += QL) AT(S.astate, AT(S.active, i)) = ARB_NORMAL;
+#ifndef MG_EXP_NO_INTEGRATE  // timing experiments only (tools/build_unit_variant.sh): bodies never move
     for (int p = sub; p < nb; p += QL) {
         const int b = quad_body(p, nb);
         AT(S.bpx, b) = AT(S.bpx, b) + (AT(S.bvx, b) + AT(S.bvbx, b)) * dt;
@@ -182,6 +183,7 @@ MG_DEV void space_step_quad(const MGState &S, const mg_library *L, int e, int su
         body_set_angle_step(S, e, b, AT(S.ba, b) + (AT(S.bw, b) + AT(S.bwb, b)) * dt);
         AT(S.bvbx, b) = 0.0; AT(S.bvby, b) = 0.0; AT(S.bwb, b) = 0.0;
     }
+#endif
     __syncthreads();   // every lane has read the scalars; bodies before the shape BBs
     if (sub == 0) { S.stamp[e] = stamp; S.curr_dt[e] = dt; S.nactive[e] = 0; }
     for (int k = sub; k < ns; k += QL) shape_update_bb(S, L, e, k);
@@ -201,8 +203,10 @@ MG_DEV void space_step_quad(const MGState &S, const mg_library *L, int e, int su
     __syncthreads();
     MG_PP(P, 3);
     const int nact = S.nactive[e];
+#ifndef MG_EXP_NO_PRESTEP    // timing experiments only: no pre-steps
     for (int i = sub; i < nact; i += QL) arbiter_prestep(S, L, e, AT(S.active, i), dt);
     static_prestep_quad<NCS, QL>(S, e, sub, dt);
+#endif
     __syncthreads();
     MG_PP(P, 4);
     // velocity integration is the identity here (no gravity, damping 1, no forces)
@@ -231,7 +235,9 @@ __device__ __forceinline__ void env_substeps_quad(const MGState &V, const mg_lib
     for (int i = 0; i < 10; i++) {
         MG_PP(P, 0);
         space_step_quad<NCS, QL, LDS_SHAPES>(V, L, ev, sub, dt, P);   // starts with a workgroup barrier
+#ifndef MG_EXP_NO_RU         // timing experiments only: no robot update after the first
         if (sub == 0 && i < 9) robot_update<true>(V, L, ev);
+#endif
     }
     __syncthreads();
 }
