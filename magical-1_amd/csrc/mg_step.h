@@ -590,6 +590,85 @@ MG_DEV void harb_apply(RegBodies<NB> &R, const MGState &S, int e, int slot) {
     }
 }
 
+// harb_apply with compile-time body slots A / B (< 0: the static body): the arbiter pairs the compile-time
+// scenes produce (robot body / finger / block against a wall or the block) touch body registers by constant
+// index instead of through one-hot selects (harb_apply: ~230 selects per contact).  The same operations in the
+// same order as harb_apply: a static side contributes velocity +0.0 and receives nothing, as there.
+template <int NB, int A, int B>
+MG_DEV void harb_apply_k(RegBodies<NB> &R, const MGState &S, int e, int slot) {
+    const double am = A >= 0 ? R.minv[A] : 0.0, ai = A >= 0 ? R.iinv[A] : 0.0;
+    const double bm = B >= 0 ? R.minv[B] : 0.0, bi = B >= 0 ? R.iinv[B] : 0.0;
+    V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
+    double friction = AT(S.au, slot);
+    int cnt = AT(S.acount, slot);
+    for (int k = 0; k < cnt; k++) {
+        double nMass = ACON(k, AC_NMASS, slot);
+        V2 r1 = v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)), r2 = v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot));
+        V2 vb1 = v2(0.0, 0.0), v1 = v2(0.0, 0.0), vb2 = v2(0.0, 0.0), v2_ = v2(0.0, 0.0);
+        if constexpr (A >= 0) {
+            vb1 = vadd(v2(R.vbx[A], R.vby[A]), vmult(vperp(r1), R.wb[A]));
+            v1 = vadd(v2(R.vx[A], R.vy[A]), vmult(vperp(r1), R.w[A]));
+        }
+        if constexpr (B >= 0) {
+            vb2 = vadd(v2(R.vbx[B], R.vby[B]), vmult(vperp(r2), R.wb[B]));
+            v2_ = vadd(v2(R.vx[B], R.vy[B]), vmult(vperp(r2), R.w[B]));
+        }
+        V2 vr = vsub(v2_, v1);
+        double vbn = vdot(vsub(vb2, vb1), n);
+        double vrn = vdot(vr, n);
+        double vrt = vdot(vr, vperp(n));
+        double jbn = (ACON(k, AC_BIAS, slot) - vbn) * nMass;
+        double jbnOld = ACON(k, AC_JB, slot);
+        double jBias = cpmax(jbnOld + jbn, 0.0);
+        ACON(k, AC_JB, slot) = jBias;
+        double jn = -(0.0 + vrn) * nMass;
+        double jnOld = ACON(k, AC_JN, slot);
+        double jnAcc = cpmax(jnOld + jn, 0.0);
+        ACON(k, AC_JN, slot) = jnAcc;
+        double jtMax = friction * jnAcc;
+        double jt = -vrt * ACON(k, AC_TMASS, slot);
+        double jtOld = ACON(k, AC_JT, slot);
+        double jtAcc = cpclamp(jtOld + jt, -jtMax, jtMax);
+        ACON(k, AC_JT, slot) = jtAcc;
+        V2 jb = vmult(n, jBias - jbnOld);
+        if constexpr (A >= 0) {
+            const V2 m = vneg(jb);
+            R.vbx[A] = R.vbx[A] + m.x * am; R.vby[A] = R.vby[A] + m.y * am; R.wb[A] = R.wb[A] + ai * vcross(r1, m);
+        }
+        if constexpr (B >= 0) {
+            R.vbx[B] = R.vbx[B] + jb.x * bm; R.vby[B] = R.vby[B] + jb.y * bm; R.wb[B] = R.wb[B] + bi * vcross(r2, jb);
+        }
+        V2 j = vrotate(n, v2(jnAcc - jnOld, jtAcc - jtOld));
+        if constexpr (A >= 0) {
+            const V2 m = vneg(j);
+            R.vx[A] = R.vx[A] + m.x * am; R.vy[A] = R.vy[A] + m.y * am; R.w[A] = R.w[A] + ai * vcross(r1, m);
+        }
+        if constexpr (B >= 0) {
+            R.vx[B] = R.vx[B] + j.x * bm; R.vy[B] = R.vy[B] + j.y * bm; R.w[B] = R.w[B] + bi * vcross(r2, j);
+        }
+    }
+}
+
+// one arbiter row of the compile-time scenes: dispatched on its (body A, body B) pair -- robot body 0 (a circle,
+// ordered before a wall), fingers 4 / 5 and the block 6 (polygons, ordered after a wall), each against a wall
+// or the block (shape_body_slot) -- to harb_apply_k; any other pair takes the select form
+template <int NB>
+MG_DEV void harb_row(RegBodies<NB> &R, const MGState &S, int e, int slot) {
+#ifndef MG_EXP_HARB_SELECT  // timing experiments only: every arbiter row through the one-hot selects
+    const int sa = AT(S.asa, slot), sb = AT(S.asb, slot);
+    if (sa == 0 && sb < 0) { harb_apply_k<NB, 0, -1>(R, S, e, slot); return; }
+    if (sa < 0 && sb == 4) { harb_apply_k<NB, -1, 4>(R, S, e, slot); return; }
+    if (sa < 0 && sb == 5) { harb_apply_k<NB, -1, 5>(R, S, e, slot); return; }
+    if constexpr (NB > 6) {
+        if (sa < 0 && sb == 6) { harb_apply_k<NB, -1, 6>(R, S, e, slot); return; }
+        if (sa == 0 && sb == 6) { harb_apply_k<NB, 0, 6>(R, S, e, slot); return; }
+        if (sa == 4 && sb == 6) { harb_apply_k<NB, 4, 6>(R, S, e, slot); return; }
+        if (sa == 5 && sb == 6) { harb_apply_k<NB, 5, 6>(R, S, e, slot); return; }
+    }
+#endif
+    harb_apply(R, S, e, slot);
+}
+
 template <int NCS, int C = 0>
 MG_DEV void rstatic_load(RegCons *q, const MGState &S, int e, double dt) {
     if constexpr (C < NCS) {
@@ -641,11 +720,29 @@ MG_DEV void static_solve(const MGState &S, int e, double dt, double dt_coef, int
 #ifdef MG_EXP_NOARBIT       // timing experiments only: no arbiter rows in the iterations
     nact = 0;
 #endif
+#ifdef MG_EXP_ARBSTAT       // statistics experiments only: substeps with live arbiters, counted in bits 12+
+    if (nact > 0) S.overflow[e] += 1 << 12;
+#endif
+#ifdef MG_ISA_MARK          // ISA reading only: comment markers around the iteration loop
+    asm volatile("; MG_ITER_BEGIN");
+#endif
 #pragma unroll 1
     for (int it = 0; it < MG_EXP_ITERS; it++) {
-        for (int i = 0; i < nact; i++) harb_apply(R, S, e, AT(S.active, i));
+        for (int i = 0; i < nact; i++) harb_row(R, S, e, AT(S.active, i));
+#ifdef MG_ISA_MARK
+        asm volatile("; MG_ROWS_BEGIN");
+#endif
         rstatic_apply<NCS>(R, q);
+#ifdef MG_EXP_ROWS2         // timing experiments only: the constraint rows twice per iteration
+        rstatic_apply<NCS>(R, q);
+#endif
+#ifdef MG_ISA_MARK
+        asm volatile("; MG_ROWS_END");
+#endif
     }
+#ifdef MG_ISA_MARK
+    asm volatile("; MG_ITER_END");
+#endif
     rb_store(R, S, e);
     rstatic_store<NCS>(q, S, e);
 }
