@@ -649,6 +649,45 @@ MG_DEV void harb_apply_k(RegBodies<NB> &R, const MGState &S, int e, int slot) {
     }
 }
 
+// harb_cached with compile-time body slots (applyCachedImpulse of one arbiter; see harb_apply_k)
+template <int NB, int A, int B>
+MG_DEV void harb_cached_k(RegBodies<NB> &R, const MGState &S, int e, int slot, double dt_coef) {
+    const double am = A >= 0 ? R.minv[A] : 0.0, ai = A >= 0 ? R.iinv[A] : 0.0;
+    const double bm = B >= 0 ? R.minv[B] : 0.0, bi = B >= 0 ? R.iinv[B] : 0.0;
+    V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
+    int cnt = AT(S.acount, slot);
+    for (int k = 0; k < cnt; k++) {
+        V2 j = vmult(vrotate(n, v2(ACON(k, AC_JN, slot), ACON(k, AC_JT, slot))), dt_coef);
+        if constexpr (A >= 0) {
+            const V2 m = vneg(j), r1 = v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot));
+            R.vx[A] = R.vx[A] + m.x * am; R.vy[A] = R.vy[A] + m.y * am; R.w[A] = R.w[A] + ai * vcross(r1, m);
+        }
+        if constexpr (B >= 0) {
+            const V2 r2 = v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot));
+            R.vx[B] = R.vx[B] + j.x * bm; R.vy[B] = R.vy[B] + j.y * bm; R.w[B] = R.w[B] + bi * vcross(r2, j);
+        }
+    }
+}
+
+// applyCachedImpulse of one arbiter of the compile-time scenes, dispatched as harb_row
+template <int NB>
+MG_DEV void harb_cached_row(RegBodies<NB> &R, const MGState &S, int e, int slot, double dt_coef) {
+    if (AT(S.astate, slot) == ARB_FIRST) return;
+#ifndef MG_EXP_HARB_SELECT
+    const int sa = AT(S.asa, slot), sb = AT(S.asb, slot);
+    if (sa == 0 && sb < 0) { harb_cached_k<NB, 0, -1>(R, S, e, slot, dt_coef); return; }
+    if (sa < 0 && sb == 4) { harb_cached_k<NB, -1, 4>(R, S, e, slot, dt_coef); return; }
+    if (sa < 0 && sb == 5) { harb_cached_k<NB, -1, 5>(R, S, e, slot, dt_coef); return; }
+    if constexpr (NB > 6) {
+        if (sa < 0 && sb == 6) { harb_cached_k<NB, -1, 6>(R, S, e, slot, dt_coef); return; }
+        if (sa == 0 && sb == 6) { harb_cached_k<NB, 0, 6>(R, S, e, slot, dt_coef); return; }
+        if (sa == 4 && sb == 6) { harb_cached_k<NB, 4, 6>(R, S, e, slot, dt_coef); return; }
+        if (sa == 5 && sb == 6) { harb_cached_k<NB, 5, 6>(R, S, e, slot, dt_coef); return; }
+    }
+#endif
+    harb_cached(R, S, e, slot, dt_coef);
+}
+
 // one arbiter row of the compile-time scenes: dispatched on its (body A, body B) pair -- robot body 0 (a circle,
 // ordered before a wall), fingers 4 / 5 and the block 6 (polygons, ordered after a wall), each against a wall
 // or the block (shape_body_slot) -- to harb_apply_k; any other pair takes the select form
@@ -711,7 +750,7 @@ MG_DEV void static_solve(const MGState &S, int e, double dt, double dt_coef, int
     RegCons q[NCS];
     rb_load(R, S, e);
     rstatic_load<NCS>(q, S, e, dt);
-    for (int i = 0; i < nact; i++) harb_cached(R, S, e, AT(S.active, i), dt_coef);
+    for (int i = 0; i < nact; i++) harb_cached_row(R, S, e, AT(S.active, i), dt_coef);
     rstatic_cached<NCS>(R, q, dt_coef);
     MG_PP(P, 5);
 #ifndef MG_EXP_ITERS        // timing experiments only (tools/build_unit_variant.sh)
