@@ -708,6 +708,117 @@ MG_DEV void harb_row(RegBodies<NB> &R, const MGState &S, int e, int slot) {
     harb_apply(R, S, e, slot);
 }
 
+// The first NARB active arbiters of a substep in registers for the 10 iterations (the compile-time scenes
+// rarely hold more: MoveToRegion has live arbiters in 3.5% of env-substeps, MoveToCorner 10%): their pair code,
+// normal, friction and contacts' pre-stepped terms are read from LDS once per substep instead of once per
+// iteration, the accumulated impulses stay in registers and are written back after the sweep.  Same operations
+// in the same order as harb_apply.
+struct RegArb {
+    int code, cnt;
+    double nx, ny, fr, nm[2], r1x[2], r1y[2], r2x[2], r2y[2], bias[2], tm[2], jb[2], jn[2], jt[2];
+};
+// pair code of an arbiter's (body A, body B) in the compile-time scenes (harb_row's cases), -1: other
+MG_DEV int arb_pair_code(int sa, int sb) {
+    if (sa == 0 && sb < 0) return 0;
+    if (sa < 0 && sb == 4) return 1;
+    if (sa < 0 && sb == 5) return 2;
+    if (sa < 0 && sb == 6) return 3;
+    if (sa == 0 && sb == 6) return 4;
+    if (sa == 4 && sb == 6) return 5;
+    if (sa == 5 && sb == 6) return 6;
+    return -1;
+}
+MG_DEV void rarb_load(RegArb &a, const MGState &S, int e, int slot) {
+    a.code = arb_pair_code(AT(S.asa, slot), AT(S.asb, slot));
+    a.cnt = AT(S.acount, slot);
+    a.nx = AT(S.anx, slot); a.ny = AT(S.any, slot); a.fr = AT(S.au, slot);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        a.nm[k] = ACON(k, AC_NMASS, slot); a.bias[k] = ACON(k, AC_BIAS, slot); a.tm[k] = ACON(k, AC_TMASS, slot);
+        a.r1x[k] = ACON(k, AC_R1X, slot); a.r1y[k] = ACON(k, AC_R1Y, slot);
+        a.r2x[k] = ACON(k, AC_R2X, slot); a.r2y[k] = ACON(k, AC_R2Y, slot);
+        a.jb[k] = ACON(k, AC_JB, slot); a.jn[k] = ACON(k, AC_JN, slot); a.jt[k] = ACON(k, AC_JT, slot);
+    }
+}
+MG_DEV void rarb_store(const RegArb &a, const MGState &S, int e, int slot) {
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+        if (k < a.cnt) { ACON(k, AC_JB, slot) = a.jb[k]; ACON(k, AC_JN, slot) = a.jn[k]; ACON(k, AC_JT, slot) = a.jt[k]; }
+}
+template <int NB, int A, int B>
+MG_DEV void rarb_apply_k(RegBodies<NB> &R, RegArb &a) {
+    const double am = A >= 0 ? R.minv[A] : 0.0, ai = A >= 0 ? R.iinv[A] : 0.0;
+    const double bm = B >= 0 ? R.minv[B] : 0.0, bi = B >= 0 ? R.iinv[B] : 0.0;
+    const V2 n = v2(a.nx, a.ny);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        if (k >= a.cnt) break;
+        const double nMass = a.nm[k];
+        V2 r1 = v2(a.r1x[k], a.r1y[k]), r2 = v2(a.r2x[k], a.r2y[k]);
+        V2 vb1 = v2(0.0, 0.0), v1 = v2(0.0, 0.0), vb2 = v2(0.0, 0.0), v2_ = v2(0.0, 0.0);
+        if constexpr (A >= 0) {
+            vb1 = vadd(v2(R.vbx[A], R.vby[A]), vmult(vperp(r1), R.wb[A]));
+            v1 = vadd(v2(R.vx[A], R.vy[A]), vmult(vperp(r1), R.w[A]));
+        }
+        if constexpr (B >= 0) {
+            vb2 = vadd(v2(R.vbx[B], R.vby[B]), vmult(vperp(r2), R.wb[B]));
+            v2_ = vadd(v2(R.vx[B], R.vy[B]), vmult(vperp(r2), R.w[B]));
+        }
+        V2 vr = vsub(v2_, v1);
+        double vbn = vdot(vsub(vb2, vb1), n);
+        double vrn = vdot(vr, n);
+        double vrt = vdot(vr, vperp(n));
+        double jbn = (a.bias[k] - vbn) * nMass;
+        double jbnOld = a.jb[k];
+        double jBias = cpmax(jbnOld + jbn, 0.0);
+        a.jb[k] = jBias;
+        double jn = -(0.0 + vrn) * nMass;
+        double jnOld = a.jn[k];
+        double jnAcc = cpmax(jnOld + jn, 0.0);
+        a.jn[k] = jnAcc;
+        double jtMax = a.fr * jnAcc;
+        double jt = -vrt * a.tm[k];
+        double jtOld = a.jt[k];
+        double jtAcc = cpclamp(jtOld + jt, -jtMax, jtMax);
+        a.jt[k] = jtAcc;
+        V2 jb = vmult(n, jBias - jbnOld);
+        if constexpr (A >= 0) {
+            const V2 m = vneg(jb);
+            R.vbx[A] = R.vbx[A] + m.x * am; R.vby[A] = R.vby[A] + m.y * am; R.wb[A] = R.wb[A] + ai * vcross(r1, m);
+        }
+        if constexpr (B >= 0) {
+            R.vbx[B] = R.vbx[B] + jb.x * bm; R.vby[B] = R.vby[B] + jb.y * bm; R.wb[B] = R.wb[B] + bi * vcross(r2, jb);
+        }
+        V2 j = vrotate(n, v2(jnAcc - jnOld, jtAcc - jtOld));
+        if constexpr (A >= 0) {
+            const V2 m = vneg(j);
+            R.vx[A] = R.vx[A] + m.x * am; R.vy[A] = R.vy[A] + m.y * am; R.w[A] = R.w[A] + ai * vcross(r1, m);
+        }
+        if constexpr (B >= 0) {
+            R.vx[B] = R.vx[B] + j.x * bm; R.vy[B] = R.vy[B] + j.y * bm; R.w[B] = R.w[B] + bi * vcross(r2, j);
+        }
+    }
+}
+// a register arbiter's row (its code is one of arb_pair_code's: rarb_ok checked it at load)
+template <int NB>
+MG_DEV void rarb_row(RegBodies<NB> &R, RegArb &a) {
+    switch (a.code) {
+    case 0: rarb_apply_k<NB, 0, -1>(R, a); break;
+    case 1: rarb_apply_k<NB, -1, 4>(R, a); break;
+    case 2: rarb_apply_k<NB, -1, 5>(R, a); break;
+    default:
+        if constexpr (NB > 6) {
+            switch (a.code) {
+            case 3: rarb_apply_k<NB, -1, 6>(R, a); break;
+            case 4: rarb_apply_k<NB, 0, 6>(R, a); break;
+            case 5: rarb_apply_k<NB, 4, 6>(R, a); break;
+            default: rarb_apply_k<NB, 5, 6>(R, a); break;
+            }
+        }
+        break;
+    }
+}
+
 template <int NCS, int C = 0>
 MG_DEV void rstatic_load(RegCons *q, const MGState &S, int e, double dt) {
     if constexpr (C < NCS) {
@@ -742,8 +853,10 @@ MG_DEV void rstatic_apply(RegBodies<NB> &R, RegCons *q) {
 // bodies of the compile-time scenes: the robot's six, plus the block's
 __host__ __device__ constexpr int static_nbodies(int ncs) { return ncs > 10 ? 7 : 6; }
 
-// applyCachedImpulse + 10 iterations of the LDS variants, register-resident
-template <int NCS>
+// applyCachedImpulse + 10 iterations of the LDS variants, register-resident; NARB arbiters in registers (the
+// 8-env form: 1 -- MoveToRegion 0.414 -> 0.392 ms, MoveToCorner 0.757 -> 0.740 ms per 2048-env chunk; 2 made
+// the MoveToCorner form spill and measured slower, and the 16-env forms spill already at 1: 0 there)
+template <int NCS, int NARB>
 MG_DEV void static_solve(const MGState &S, int e, double dt, double dt_coef, int nact, MGProf &P) {
     constexpr int NB = static_nbodies(NCS);
     RegBodies<NB> R;
@@ -765,9 +878,30 @@ MG_DEV void static_solve(const MGState &S, int e, double dt, double dt_coef, int
 #ifdef MG_ISA_MARK          // ISA reading only: comment markers around the iteration loop
     asm volatile("; MG_ITER_BEGIN");
 #endif
+    // the first NARB arbiters in registers when their pairs are compile-time ones (the rest through LDS)
+    RegArb ra[NARB > 0 ? NARB : 1];
+    int nreg = 0;
+    if constexpr (NARB > 0) {
+#pragma unroll
+        for (int i = 0; i < NARB; i++) {
+            ra[i].code = -1; ra[i].cnt = 0;
+            if (i < nact) rarb_load(ra[i], S, e, AT(S.active, i));
+        }
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < NARB; i++) {
+            if (i < nact && ok && ra[i].code >= 0 && (NB > 6 || ra[i].code <= 2)) nreg = i + 1;
+            else ok = false;
+        }
+    }
 #pragma unroll 1
     for (int it = 0; it < MG_EXP_ITERS; it++) {
-        for (int i = 0; i < nact; i++) harb_row(R, S, e, AT(S.active, i));
+        if constexpr (NARB > 0) {
+#pragma unroll
+            for (int i = 0; i < NARB; i++)
+                if (i < nreg) rarb_row(R, ra[i]);
+        }
+        for (int i = nreg; i < nact; i++) harb_row(R, S, e, AT(S.active, i));
 #ifdef MG_ISA_MARK
         asm volatile("; MG_ROWS_BEGIN");
 #endif
@@ -782,6 +916,11 @@ MG_DEV void static_solve(const MGState &S, int e, double dt, double dt_coef, int
 #ifdef MG_ISA_MARK
     asm volatile("; MG_ITER_END");
 #endif
+    if constexpr (NARB > 0) {
+#pragma unroll
+        for (int i = 0; i < NARB; i++)
+            if (i < nreg) rarb_store(ra[i], S, e, AT(S.active, i));
+    }
     rb_store(R, S, e);
     rstatic_store<NCS>(q, S, e);
 }

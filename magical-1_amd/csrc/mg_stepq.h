@@ -211,7 +211,7 @@ MG_DEV void space_step_quad(const MGState &S, const mg_library *L, int e, int su
     MG_PP(P, 4);
     // velocity integration is the identity here (no gravity, damping 1, no forces)
     const double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
-    if (sub == 0) static_solve<NCS>(S, e, dt, dt_coef, nact, P);
+    if (sub == 0) static_solve<NCS, (QL >= 8 ? 1 : 0)>(S, e, dt, dt_coef, nact, P);   // NARB: see static_solve
     MG_PP(P, 6);
 }
 
