@@ -1318,18 +1318,40 @@ MG_DEV void xarb_cached_k(LaneBodies &R, RobotV &V, int lane, const MGState &S, 
         xapply<KB>(R, V, lane, b, j, v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot)));
     }
 }
+// one side of an arbiter row, gathered once per row (not per contact) into wave-uniform registers: velocities and
+// masses of a robot body (RobotV slot K >= 0) or of a block body (readlane from its lane), zeros for the static
+// body (b < 0, never written back); bias velocities always live in the body's lane
+struct XSide { double vx, vy, w, vbx, vby, wb, minv, iinv; };
+template <int K>
+MG_DEV XSide xside_get(const LaneBodies &R, const RobotV &V, int b) {
+    XSide x;
+    x.vx = xget<K>(R.vx, V.vx, b); x.vy = xget<K>(R.vy, V.vy, b); x.w = xget<K>(R.w, V.w, b);
+    x.minv = xget<K>(R.minv, V.minv, b); x.iinv = xget<K>(R.iinv, V.iinv, b);
+    x.vbx = lget(R.vbx, b); x.vby = lget(R.vby, b); x.wb = lget(R.wb, b);
+    return x;
+}
+template <int K>
+MG_DEV void xside_put(LaneBodies &R, RobotV &V, int b, int lane, const XSide &x) {
+    if (K < 0 && b < 0) return;
+    xput<K>(R.vx, V.vx, b, lane, x.vx); xput<K>(R.vy, V.vy, b, lane, x.vy); xput<K>(R.w, V.w, b, lane, x.w);
+    lput(R.vbx, b, lane, x.vbx); lput(R.vby, b, lane, x.vby); lput(R.wb, b, lane, x.wb);
+}
 template <int KA, int KB>
 MG_DEV void xarb_apply_k(LaneBodies &R, RobotV &V, int lane, const MGState &S, int e, int slot, int a, int b) {
     V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
     double friction = AT(S.au, slot);
     const int cnt = ufirst(AT(S.acount, slot));
+    // a and b are distinct bodies (or the static body), so each side's values can be carried across the row's
+    // contacts in registers: the same reads and writes as per-contact lget / lput, in the same order
+    XSide A = xside_get<KA>(R, V, a), B = xside_get<KB>(R, V, b);
+    const bool da = KA >= 0 || a >= 0, db = KB >= 0 || b >= 0;   // sides that receive impulses
     for (int k = 0; k < cnt; k++) {
         double nMass = ACON(k, AC_NMASS, slot);
         V2 r1 = v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)), r2 = v2(ACON(k, AC_R2X, slot), ACON(k, AC_R2Y, slot));
-        V2 vb1 = vadd(v2(lget(R.vbx, a), lget(R.vby, a)), vmult(vperp(r1), lget(R.wb, a)));
-        V2 vb2 = vadd(v2(lget(R.vbx, b), lget(R.vby, b)), vmult(vperp(r2), lget(R.wb, b)));
-        V2 v1 = vadd(v2(xget<KA>(R.vx, V.vx, a), xget<KA>(R.vy, V.vy, a)), vmult(vperp(r1), xget<KA>(R.w, V.w, a)));
-        V2 v2_ = vadd(v2(xget<KB>(R.vx, V.vx, b), xget<KB>(R.vy, V.vy, b)), vmult(vperp(r2), xget<KB>(R.w, V.w, b)));
+        V2 vb1 = vadd(v2(A.vbx, A.vby), vmult(vperp(r1), A.wb));
+        V2 vb2 = vadd(v2(B.vbx, B.vby), vmult(vperp(r2), B.wb));
+        V2 v1 = vadd(v2(A.vx, A.vy), vmult(vperp(r1), A.w));
+        V2 v2_ = vadd(v2(B.vx, B.vy), vmult(vperp(r2), B.w));
         V2 vr = vsub(v2_, v1);
         double vbn = vdot(vsub(vb2, vb1), n);
         double vrn = vdot(vr, n);
@@ -1346,12 +1368,20 @@ MG_DEV void xarb_apply_k(LaneBodies &R, RobotV &V, int lane, const MGState &S, i
         double jtAcc = cpclamp(jtOld + jt, -jtMax, jtMax);
         if (lane == 0) { ACON(k, AC_JB, slot) = jBias; ACON(k, AC_JN, slot) = jnAcc; ACON(k, AC_JT, slot) = jtAcc; }
         V2 jb = vmult(n, jBias - jbnOld);
-        xapply_bias<KA>(R, V, lane, a, vneg(jb), r1);
-        xapply_bias<KB>(R, V, lane, b, jb, r2);
+        if (a >= 0) {   // xapply_bias: bias velocities of a non-static side
+            const V2 m = vneg(jb);
+            A.vbx = A.vbx + m.x * A.minv; A.vby = A.vby + m.y * A.minv; A.wb = A.wb + A.iinv * vcross(r1, m);
+        }
+        if (b >= 0) { B.vbx = B.vbx + jb.x * B.minv; B.vby = B.vby + jb.y * B.minv; B.wb = B.wb + B.iinv * vcross(r2, jb); }
         V2 j = vrotate(n, v2(jnAcc - jnOld, jtAcc - jtOld));
-        xapply<KA>(R, V, lane, a, vneg(j), r1);
-        xapply<KB>(R, V, lane, b, j, r2);
+        if (da) {
+            const V2 m = vneg(j);
+            A.vx = A.vx + m.x * A.minv; A.vy = A.vy + m.y * A.minv; A.w = A.w + A.iinv * vcross(r1, m);
+        }
+        if (db) { B.vx = B.vx + j.x * B.minv; B.vy = B.vy + j.y * B.minv; B.w = B.w + B.iinv * vcross(r2, j); }
     }
+    xside_put<KA>(R, V, a, lane, A);
+    xside_put<KB>(R, V, b, lane, B);
 }
 // Arbiter rows dispatched on their bodies' robot slots (uniform branches, so every RobotV access has a constant
 // slot): only the bodies that carry shapes can be in contact -- the robot body (slot 0) and the fingers (4, 5)

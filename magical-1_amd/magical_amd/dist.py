@@ -339,9 +339,7 @@ class ShardedVecEnv:
             dev_name = device or f"cuda:{torch.cuda.current_device()}"
             seeds = shard_seeds(envs_per_rank, self.rank, base_seed)
             if chunks > 1:   # the pipelined env pool (magical_amd.pipeline): chunks overlap under the exchange
-                if spec.task == "PickAndPlace":
-                    raise ValueError("ShardedVecEnv: a pipelined PickAndPlace shard would gather its target before "
-                                     "the chunks' resets wrote it")
+                # (PickAndPlace: the pool copies its target into the packed view on each chunk's stream)
                 from .pipeline import PipelinedVecEnv
                 vec = PipelinedVecEnv(env_name, envs_per_rank, chunks=chunks, device=dev_name, seeds=seeds,
                                       max_episode_steps=max_episode_steps, window=False)
@@ -432,8 +430,13 @@ class ShardedVecEnv:
     def _finish_outputs(self, b):
         # PickAndPlace's target is written by the simulator only at reset: copy the env's persistent
         # buffer into this step's packed views (never gather a stale or unwritten target)
-        if self.layout.fields[-1][0] == "target":
+        # (a pipelined pool copies its target into the bound "target" view itself, on each chunk's stream right
+        # after the chunk's step: PipelinedVecEnv.bind_outputs)
+        if self.layout.fields[-1][0] == "target" and not self._pooled():
             self.layout.views(self.send[b])["target"].copy_(self.vec.target)
+
+    def _pooled(self):
+        return self.comm_stream is not None and hasattr(self.vec, "step_events")
 
     def _launch(self, b, all_fresh):
         send, recv, stacks = self.send[b], self.recv[b], self.stacks[b]

@@ -83,6 +83,11 @@ class PipelinedVecEnv:
         self.t = 0
         self.reset_count = 0      # explicit reset() calls (magical_amd.dist checks its frame rings against it)
         self.target = self.buffers.get("target")
+        # the observation's float32 target columns, converted on each chunk's stream right after its step (a
+        # conversion on the caller's stream inside step() would read the target before the chunk wrote it)
+        self.target_f = None if self.target is None else torch.zeros(self.target.shape, dtype=torch.float32,
+                                                                     device=self.device)
+        self._target_out = None   # bind_outputs' "target" view (magical_amd.dist's packed buffer)
         self._last = []           # the chunk streams' events of the last step() (magical_amd.dist waits on them)
 
     # -- ordering ------------------------------------------------------------------
@@ -118,12 +123,19 @@ class PipelinedVecEnv:
         for k, sim in enumerate(self.sims):
             sim.bind_outputs({key: v[b[k]:b[k + 1]] for key, v in views.items() if key != "target"},
                              frames_only=frames_only)
+        # PickAndPlace: the pool's persistent target is copied into views["target"] on each chunk's stream right
+        # after the chunk's step (reset: on the caller's stream), so the view is complete when the chunk is
+        self._target_out = views.get("target") if self.target is not None else None
 
     # -- API -----------------------------------------------------------------------
     def reset(self, mask=None):
         self.wait()
         for k, sim in enumerate(self.sims):
             sim.reset(None if mask is None else mask[self.bounds[k]:self.bounds[k + 1]])
+        if self.target_f is not None:   # the resets ran on the caller's stream
+            self.target_f.copy_(self.target)
+            if self._target_out is not None:
+                self._target_out.copy_(self.target)
         self.reset_count += 1
         self._last = []
         self._fork()
@@ -144,6 +156,10 @@ class PipelinedVecEnv:
         for k, (sim, st) in enumerate(zip(self.sims, self.streams)):
             with torch.cuda.stream(st):
                 sim.step(self.abuf[slot, b[k]:b[k + 1]])
+                if self.target_f is not None:
+                    self.target_f[b[k]:b[k + 1]].copy_(self.target[b[k]:b[k + 1]])
+                    if self._target_out is not None:
+                        self._target_out[b[k]:b[k + 1]].copy_(self.target[b[k]:b[k + 1]])
             ev = torch.cuda.Event()
             ev.record(st)
             self.done_ev[k][slot] = ev
@@ -163,8 +179,8 @@ class PipelinedVecEnv:
         out = collections.OrderedDict([("allo", allo), ("ego", ego)])
         if self.sims[0]._chw:
             out = collections.OrderedDict((k, v.permute(0, 3, 1, 2)) for k, v in out.items())
-        if "target" in self.buffers:
-            t = self.buffers["target"].to(torch.float32)
+        if self.target_f is not None:
+            t = self.target_f
             out["target_type"], out["target_colour"], out["target_position"] = t[:, 0:1], t[:, 1:2], t[:, 2:4]
         if past is not None:
             out["past_obs"] = past.permute(0, 3, 1, 2) if self.sims[0]._chw else past

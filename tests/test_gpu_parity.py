@@ -856,7 +856,8 @@ GATHER_GPU_CASES = [("MoveToRegion-Demo-LoRes4E-v0", "frames", 40, {}),
                     ("MoveToCorner-Demo-LoRes3EA-v0", "frames", 15, {}),
                     ("MoveToCorner-Demo-LoRes4A-v0", "frames", 15, {}),
                     ("MoveToCorner-Demo-LoRes4A-v0", "frames", 15, {"chunks": 2}),
-                    ("PickAndPlace-Demo-LoRes4E-v0", "frames", 15, {})]
+                    ("PickAndPlace-Demo-LoRes4E-v0", "frames", 15, {}),
+                    ("PickAndPlace-Demo-LoRes4E-v0", "frames", 15, {"chunks": 2})]
 
 
 @pytest.mark.gpu
