@@ -1309,9 +1309,8 @@ MG_DEV void xapply_bias(LaneBodies &R, RobotV &V, int lane, int b, V2 j, V2 r) {
 }
 template <int KA, int KB>
 MG_DEV void xarb_cached_k(LaneBodies &R, RobotV &V, int lane, const MGState &S, int e, int slot, int a, int b,
-                          double dt_coef) {
+                          int cnt, double dt_coef) {
     V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
-    const int cnt = ufirst(AT(S.acount, slot));
     for (int k = 0; k < cnt; k++) {
         V2 j = vmult(vrotate(n, v2(ACON(k, AC_JN, slot), ACON(k, AC_JT, slot))), dt_coef);
         xapply<KA>(R, V, lane, a, vneg(j), v2(ACON(k, AC_R1X, slot), ACON(k, AC_R1Y, slot)));
@@ -1337,10 +1336,10 @@ MG_DEV void xside_put(LaneBodies &R, RobotV &V, int b, int lane, const XSide &x)
     lput(R.vbx, b, lane, x.vbx); lput(R.vby, b, lane, x.vby); lput(R.wb, b, lane, x.wb);
 }
 template <int KA, int KB>
-MG_DEV void xarb_apply_k(LaneBodies &R, RobotV &V, int lane, const MGState &S, int e, int slot, int a, int b) {
+MG_DEV void xarb_apply_k(LaneBodies &R, RobotV &V, int lane, const MGState &S, int e, int slot, int a, int b,
+                         int cnt) {
     V2 n = v2(AT(S.anx, slot), AT(S.any, slot));
     double friction = AT(S.au, slot);
-    const int cnt = ufirst(AT(S.acount, slot));
     // a and b are distinct bodies (or the static body), so each side's values can be carried across the row's
     // contacts in registers: the same reads and writes as per-contact lget / lput, in the same order
     XSide A = xside_get<KA>(R, V, a), B = xside_get<KB>(R, V, b);
@@ -1388,13 +1387,21 @@ MG_DEV void xarb_apply_k(LaneBodies &R, RobotV &V, int lane, const MGState &S, i
 // -- and robot shapes never collide with each other (one shape group), so (a, b) is one of block / robot
 // body / finger with a block or the static body.  Any other pair would be a scene outside the compiled robot
 // rows: flagged (error 32), never expected.
+// Active arbiter i's slot, bodies, contact count and first-step flag packed into one int held by lane i
+// (arb_pack, built once per substep after the arbiter updates): a row reads them with one readlane instead of
+// two dependent LDS round trips (active[i], then the slot's fields) per row and iteration.
+MG_DEV int arb_pack(const MGState &S, int e, int i) {
+    const int slot = AT(S.active, i);
+    return slot | ((AT(S.asa, slot) + 1) << 8) | ((AT(S.asb, slot) + 1) << 12) | (AT(S.acount, slot) << 16) |
+           ((AT(S.astate, slot) == ARB_FIRST ? 1 : 0) << 20);
+}
 template <bool CACHED>
-MG_DEV void xarb_row(LaneBodies &R, RobotV &V, int rb0, int lane, const MGState &S, int e, int slot, double x) {
-    if (CACHED && ufirst(AT(S.astate, slot)) == ARB_FIRST) return;
-    const int a = ufirst(AT(S.asa, slot)), b = ufirst(AT(S.asb, slot));
+MG_DEV void xarb_row(LaneBodies &R, RobotV &V, int rb0, int lane, const MGState &S, int e, int pk, double x) {
+    if (CACHED && ((pk >> 20) & 1)) return;
+    const int slot = pk & 255, a = ((pk >> 8) & 15) - 1, b = ((pk >> 12) & 15) - 1, cnt = (pk >> 16) & 15;
     const int ka = is_rob(a, rb0) ? a - rb0 : -1, kb = is_rob(b, rb0) ? b - rb0 : -1;
-#define XROW(KA, KB) do { if (CACHED) xarb_cached_k<KA, KB>(R, V, lane, S, e, slot, a, b, x); \
-                          else xarb_apply_k<KA, KB>(R, V, lane, S, e, slot, a, b); } while (0)
+#define XROW(KA, KB) do { if (CACHED) xarb_cached_k<KA, KB>(R, V, lane, S, e, slot, a, b, cnt, x); \
+                          else xarb_apply_k<KA, KB>(R, V, lane, S, e, slot, a, b, cnt); } while (0)
     if (ka < 0 && kb < 0) XROW(-1, -1);
     else if (kb < 0 && ka == 0) XROW(0, -1);
     else if (kb < 0 && ka == 4) XROW(4, -1);
@@ -1681,7 +1688,8 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
             V.jacc2[k] = static_cons(k).type == MG_C_PIVOT ? CPA(CP_JACC2, rc0 + k) : 0.0;
             V.twrn[k] = static_cons(k).type == MG_C_SPRING ? CPA(CP_TWRN, rc0 + k) : 0.0;
         }
-        for (int i = 0; i < unact; i++) xarb_row<true>(R, V, rb0, lane, S, e, ufirst(AT(S.active, i)), dt_coef);
+        const int apk = lane < unact ? arb_pack(S, e, lane) : 0;   // active arbiter `lane` (arb_pack)
+        for (int i = 0; i < unact; i++) xarb_row<true>(R, V, rb0, lane, S, e, __builtin_amdgcn_readlane(apk, i), dt_coef);
         if (G.n > 0) {
             lground_cached(R, S, e, G.c0, dt_coef);
             if (G.n > 1) lground_cached(R, S, e, G.c1, dt_coef);
@@ -1691,7 +1699,10 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
 #pragma unroll 1
         for (int it = 0; it < MG_EXP_COOP_ITERS; it++) {
 #ifndef MG_EXP_COOP_NOARB
-            for (int i = 0; i < unact; i++) xarb_row<false>(R, V, rb0, lane, S, e, ufirst(AT(S.active, i)), 0.0);
+            for (int i = 0; i < unact; i++) xarb_row<false>(R, V, rb0, lane, S, e, __builtin_amdgcn_readlane(apk, i), 0.0);
+#endif
+#ifdef MG_EXP_COOP_ARB2      // timing experiments only: the arbiter rows twice per iteration
+            for (int i = 0; i < unact; i++) xarb_row<false>(R, V, rb0, lane, S, e, __builtin_amdgcn_readlane(apk, i), 0.0);
 #endif
 #ifndef MG_EXP_COOP_NOGROUND
             if (G.n > 0) {
@@ -1700,6 +1711,9 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
             }
 #endif
 #ifndef MG_EXP_COOP_NOCONS
+            rrows_apply(V, S, e, rc0, dt);
+#endif
+#ifdef MG_EXP_COOP_RR2       // timing experiments only: the robot rows twice per iteration
             rrows_apply(V, S, e, rc0, dt);
 #endif
         }
