@@ -384,10 +384,12 @@ int mg_create(const mg_config *cfg, mg_sim **out) {
     if (const char *mt = getenv("MG_DEBUG_MAX_TRIES")) s->S.max_tries = atoi(mt) > 0 ? atoi(mt) : 10000; // tests only
     s->reset_waves = getenv("MG_RESET_WAVES") ? atoi(getenv("MG_RESET_WAVES")) : 0;
     s->no_fused_reset = getenv("MG_FUSED_RESET") && atoi(getenv("MG_FUSED_RESET")) == 0;
-    // the shadow's next layouts run beside the step stream's kernels: 512 wavefronts scanning the pending mask
-    // instead of one 352-VGPR wavefront per env, most of which only exit (ClusterColour 1.458 -> 1.468 M,
-    // MatchRegions 1.329 -> 1.358 M env-steps/s, same box; the in-place robot-scene resets gained nothing)
-    s->reset_waves_shadow = getenv("MG_RESET_WAVES_SHADOW") ? atoi(getenv("MG_RESET_WAVES_SHADOW")) : 512;
+    // the shadow's next layouts run beside the step stream's kernels: 256 wavefronts scanning the pending mask
+    // instead of one 352-VGPR wavefront per env, most of which only exit (512: ClusterColour 1.458 -> 1.468 M,
+    // MatchRegions 1.329 -> 1.358 M env-steps/s, same box; the in-place robot-scene resets gained nothing).
+    // Round 5: 256 -- fewer 352-VGPR wavefronts holding SIMDs beside the render -- MatchRegions 1.375 -> 1.393 M,
+    // ClusterColour unchanged; 64 makes a wavefront's serial run of layouts outlast the step (MatchRegions 1.11 M)
+    s->reset_waves_shadow = getenv("MG_RESET_WAVES_SHADOW") ? atoi(getenv("MG_RESET_WAVES_SHADOW")) : 256;
     if (const char *rr = getenv("MG_DEBUG_RENDER_RETRY")) s->force_render_retry = atoi(rr);                 // tests only
     else s->force_render_retry = 0;
     s->scache_mode = getenv("MG_DEBUG_SCACHE") ? atoi(getenv("MG_DEBUG_SCACHE")) : 0;                    // tests only
