@@ -2,10 +2,6 @@
 #include "mg_launch.h"
 #include "mg_render.h"
 
-#ifndef RG_M2T
-#define RG_M2T 1
-#endif
-
 hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderOut &ro, int mode, hipStream_t st) {
     const dim3 grid(S.n_envs, 2), blk(RG_THREADS);
     RenderOut r = ro;
@@ -26,31 +22,31 @@ hipError_t mg_launch_render(const MGState &S, const mg_library *L, const RenderO
     // of MatchRegions-TestAll's, whose frames then pay a launch more and measured slower (3.30 -> 3.59 ms), so
     // the other tasks start at medium-1.
     r.retry_in = 1; r.retry_out = 1;
-#define RG_LAUNCH_CLASS(CLS)                                                                                  \
-    do {                                                                                                      \
-        if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<CLS>, 0>), grid, blk, 0, st, S, L, r);   \
-        else if (mode == 2) hipLaunchKernelGGL((render_kernel<RenderSmem<CLS>, 2>), grid, blk, 0, st, S, L, r); \
-        else hipLaunchKernelGGL((render_kernel<RenderSmem<CLS>, 1>), grid, blk, 0, st, S, L, r);             \
-        const hipError_t e = hipGetLastError();                                                               \
-        if (e != hipSuccess) return e;                                                                        \
-    } while (0)
-    if (r.first_level == 0) RG_LAUNCH_CLASS(RG_MEDIUM0);
+    hipError_t e;
+    if (r.first_level == 0) {
+        if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM0>, 0>), grid, blk, 0, st, S, L, r);
+        else if (mode == 2) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM0>, 2>), grid, blk, 0, st, S, L, r);
+        else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM0>, 1>), grid, blk, 0, st, S, L, r);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     r.cls_level = 1;
-    RG_LAUNCH_CLASS(RG_MEDIUM1);
-#if RG_M2T
-    // medium-2t (6 workgroups/CU): MatchRegions-TestAll's scenes beyond medium-1 (8.8% of its (env, view)
-    // pairs, geoms > 48) fit in one round of the chip's workgroup slots instead of 1.1 rounds of medium-2's 5/CU
+    if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM1>, 0>), grid, blk, 0, st, S, L, r);
+    else if (mode == 2) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM1>, 2>), grid, blk, 0, st, S, L, r);
+    else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM1>, 1>), grid, blk, 0, st, S, L, r);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
     r.cls_level = 2;
-    RG_LAUNCH_CLASS(RG_MEDIUM2T);
-    r.cls_level = 3;
-#else
-    r.cls_level = 2;
-#endif
-    RG_LAUNCH_CLASS(RG_MEDIUM2);
-    r.retry_out = 0; r.cls_level++;
-    RG_LAUNCH_CLASS(RG_LARGE);
-#undef RG_LAUNCH_CLASS
-    return hipSuccess;
+    if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM2>, 0>), grid, blk, 0, st, S, L, r);
+    else if (mode == 2) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM2>, 2>), grid, blk, 0, st, S, L, r);
+    else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_MEDIUM2>, 1>), grid, blk, 0, st, S, L, r);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    r.retry_out = 0; r.cls_level = 3;
+    if (mode == 0) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_LARGE>, 0>), grid, blk, 0, st, S, L, r);
+    else if (mode == 2) hipLaunchKernelGGL((render_kernel<RenderSmem<RG_LARGE>, 2>), grid, blk, 0, st, S, L, r);
+    else hipLaunchKernelGGL((render_kernel<RenderSmem<RG_LARGE>, 1>), grid, blk, 0, st, S, L, r);
+    return hipGetLastError();
 }
 
 // LoRes3EA (benchmarks/__init__.py lores_ea_entry_point: FlattenFrameStack with allo depth 1, ego
