@@ -771,12 +771,12 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         atomicMax(&g_prof[52], (unsigned long long)G); atomicMax(&g_prof[53], (unsigned long long)NV);
         atomicMax(&g_prof[54], (unsigned long long)sm.ndash); atomicMax(&g_prof[55], (unsigned long long)sm.nsedge);
         atomicMax(&g_prof[56], nb);
-        if (NV > 768) atomicAdd(&g_prof[57], 1ull);
-        if (NV > 896) atomicAdd(&g_prof[58], 1ull);
-        if (nb > 1536) atomicAdd(&g_prof[59], 1ull);
-        if (G > 48) atomicAdd(&g_prof[60], 1ull);
-        if (sm.ndash > 128) atomicAdd(&g_prof[61], 1ull);
-        if (sm.nsedge > 512) atomicAdd(&g_prof[62], 1ull);
+        if (G > 48) atomicAdd(&g_prof[57], 1ull);
+        if (G > 64) atomicAdd(&g_prof[58], 1ull);
+        if (G > 72) atomicAdd(&g_prof[59], 1ull);
+        if (NV > 1168) atomicAdd(&g_prof[60], 1ull);
+        if (nb > 2080) atomicAdd(&g_prof[61], 1ull);
+        if (sm.ndash > 128 || sm.nsedge > 712) atomicAdd(&g_prof[62], 1ull);
         atomicAdd(&g_prof[63], 1ull);
     }
 #endif

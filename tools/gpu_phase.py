@@ -54,8 +54,8 @@ for view, base in (("allo", 0), ("ego", 16)):
         print(f"   {nm:22s} {v[base + 5 + i] / (steps * n):10.1f} per WG (sum over bands)")
 if v[63]:
     print(f"render scene sizes over {v[63]} (env, view) renders: max geoms {v[52]}, vertices {v[53]}, dash lines "
-          f"{v[54]}, solid edges {v[55]}, bin entries {v[56]}; above caps: NV>768 {v[57]}, NV>896 {v[58]}, "
-          f"bins>1536 {v[59]}, geoms>48 {v[60]}, dashes>128 {v[61]}, sedges>512 {v[62]}")
+          f"{v[54]}, solid edges {v[55]}, bin entries {v[56]}; above caps: geoms>48 {v[57]}, geoms>64 {v[58]}, "
+          f"geoms>72 {v[59]}, NV>1168 {v[60]}, bins>2080 {v[61]}, dashes>128 or sedges>712 {v[62]}")
 tot = sum(v[32:42])
 # one timer per workgroup (its first lane): the robot scenes' quad forms run blk envs per workgroup (16, or 8 below
 # 16 envs per CU), the cooperative form one env per workgroup
