@@ -925,6 +925,9 @@ MG_DEV void static_solve(const MGState &S, int e, double dt, double dt_coef, int
     rstatic_store<NCS>(q, S, e);
 }
 
+#ifndef MG_COOP_COMPACT
+#define MG_COOP_COMPACT 1
+#endif
 // ---- cpSpaceStep -----------------------------------------------------------
 // one lane per env on the HBM state (variant 0, scenes beyond the LDS forms' caps): runtime constraint lists
 MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, MGProf &P) {
@@ -1561,7 +1564,110 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
     for (int k = lane; k < ns; k += 64) shape_update_bb(S, L, e, k);
     __syncthreads();
     MG_PP(P, 1);
-    // broadphase + narrowphase: pair p (canonical order) on lane p mod 64
+    // broadphase + narrowphase in canonical pair order (shape i's walls 0..3, then shapes j > i).
+#if MG_COOP_COMPACT
+    // Pass 1 tests every candidate pair, pair p on lane p mod 64 (BB, filters, exact separating-axis skip); the
+    // pairs that need collide() are compacted in canonical order -- the q-th such pair to lane q (lane q selects
+    // the bit of its rank in the chunk's ballot mask) -- so pass 2 runs collide() once for up to 64 of them (one call site) instead of once per 64-pair chunk
+    // that holds any.  Lane 0 then applies the arbiter updates in canonical order, as before.
+    const int total = pair_row_off(ns, ns);
+    auto decode = [&](int p, int &i, int &r) {
+        int lo = 0, hi = ns - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (pair_row_off(mid, ns) <= p) lo = mid; else hi = mid - 1;
+        }
+        i = lo;
+        r = p - pair_row_off(i, ns);
+    };
+    for (int round0 = 0;; round0 += 64) {   // hits [round0, round0 + 64) of the substep's canonical hit list
+        int mine = 0;                        // 1 + the pair index of this lane's hit in the round (0: none)
+        int seen = 0;                        // hits of the chunks tested so far (wave-uniform)
+        for (int base = 0; base < total; base += 64) {
+            const int p = base + lane;
+            bool hit = false;
+            if (p < total) {
+                int i, r;
+                decode(p, i, r);
+                const double al = AT(S.sbbl, i), ab = AT(S.sbbb, i), ar = AT(S.sbbr, i), at = AT(S.sbbt, i);
+                if (r < 4) {
+                    double wl, wb, wr, wt;
+                    wall_bb(r, wl, wb, wr, wt);
+                    hit = al <= wr && wl <= ar && ab <= wt && wb <= at && !(AT(S.sgroup, i) & MG_GROUP_OFF);
+                } else {
+                    const int j = i + 1 + (r - 4);
+                    const int gi = AT(S.sgroup, i), gj = AT(S.sgroup, j);
+                    hit = al <= AT(S.sbbr, j) && AT(S.sbbl, j) <= ar && ab <= AT(S.sbbt, j) && AT(S.sbbb, j) <= at &&
+                          AT(S.sbody, j) != AT(S.sbody, i) && !(gi != 0 && gi == gj) && !((gi | gj) & MG_GROUP_OFF) &&
+                          !surely_apart(S, L, e, i, j);
+                }
+            }
+            const uint64_t m = __ballot(hit);
+            const int nm = (int)__popcll(m);
+            // lane q takes the hit of rank round0 + q: the k-th set bit of this chunk's mask, if it is here
+            const int k = round0 + lane - seen;
+            if (k >= 0 && k < nm) {
+                int lo = 0, hi = 63;   // smallest bit position whose prefix holds k + 1 hits
+#pragma unroll
+                for (int it = 0; it < 6; it++) {
+                    const int mid = (lo + hi) >> 1;
+                    const uint64_t pre = mid == 63 ? ~0ull : ((2ull << mid) - 1ull);
+                    if ((int)__popcll(m & pre) > k) hi = mid; else lo = mid + 1;
+                }
+                mine = base + lo + 1;
+            }
+            seen += nm;
+        }
+        int i = 0, j = 0;
+        Collision info;
+        info.count = 0;
+        if (mine) {
+            int r;
+            decode(mine - 1, i, r);
+            ShapeW A, B;
+            load_shape(S, L, e, i, (uint64_t)AT(S.shash, i), A);
+            if (r < 4) { j = -1 - r; load_wall(r, B); }
+            else { j = i + 1 + (r - 4); load_shape(S, L, e, j, (uint64_t)AT(S.shash, j), B); }
+            collide(A, B, info);   // the one call site
+        }
+        uint64_t m = __ballot(info.count > 0);
+#ifdef MG_PROFILE
+        P.acc[10] += (unsigned long long)__popcll(__ballot(mine != 0));
+        P.acc[11] += (unsigned long long)__popcll(m);
+#endif
+        MG_PP(P, 8);
+        while (m) { // hits in lane order = canonical pair order
+            const int src = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            Collision c;
+            c.count = __builtin_amdgcn_readlane(info.count, src);
+            c.n = v2(rl_d(info.n.x, src), rl_d(info.n.y, src));
+            for (int k = 0; k < 2; k++) {
+                c.p1[k] = v2(rl_d(info.p1[k].x, src), rl_d(info.p1[k].y, src));
+                c.p2[k] = v2(rl_d(info.p2[k].x, src), rl_d(info.p2[k].y, src));
+                c.hash[k] = rl_u64(info.hash[k], src);
+            }
+            const int si = __builtin_amdgcn_readlane(i, src), sj = __builtin_amdgcn_readlane(j, src);
+            if (lane == 0) {
+                ShapeW A, B; // arbiter_update reads the shapes' types and bodies only
+                A.type = AT(S.spoly, si) < 0 ? WS_CIRCLE : WS_POLY;
+                A.body = AT(S.sbody, si);
+                double ub;
+                int key;
+                if (sj < 0) {
+                    B.type = WS_SEGMENT; B.body = -1; ub = 0.8; key = si * 128 + 100 + (-1 - sj);
+                } else {
+                    B.type = AT(S.spoly, sj) < 0 ? WS_CIRCLE : WS_POLY; B.body = AT(S.sbody, sj);
+                    ub = AT(S.su, sj); key = si * 128 + sj;
+                }
+                arbiter_update(S, L, e, key, A, B, AT(S.su, si), ub, c);
+            }
+        }
+        MG_PP(P, 9);
+        if (seen <= round0 + 64) break;   // every hit of the substep has been collided
+    }
+#else
+    // pair p (canonical order) on lane p mod 64
     const int total = pair_row_off(ns, ns);
     for (int base = 0; base < total; base += 64) {
         const int p = base + lane;
@@ -1639,6 +1745,7 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
         }
         MG_PP(P, 9);
     }
+#endif
     __syncthreads();
     MG_PP(P, 2);
     for (int i = lane; i < S.arb_cap; i += 64) { // cached arbiter filter
