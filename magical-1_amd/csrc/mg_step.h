@@ -219,6 +219,10 @@ __host__ __device__ constexpr ConsDesc static_cons(int c) {
 }
 // ---- arbiters ------------------------------------------------------------
 // (ta, ba) / (tb, bb): world-shape type and body of the pair's shapes A / B in broadphase order
+// arbiter_update_t with the slot search done by the caller: slot = the first slot holding key (-1: none),
+// free_slot = the first empty slot (used only when slot < 0)
+MG_DEV void arbiter_update_found(const MGState &S, const mg_library *L, int e, int key, int ta, int ba, int tb,
+                                 int bb, double ua, double ub, const Collision &info, int slot, int free_slot);
 MG_DEV void arbiter_update_t(const MGState &S, const mg_library *L, int e, int key, int ta, int ba, int tb, int bb,
                              double ua, double ub, const Collision &info) {
     int na = S.arb_cap, slot = -1, free_slot = -1;
@@ -227,6 +231,10 @@ MG_DEV void arbiter_update_t(const MGState &S, const mg_library *L, int e, int k
         if (k == key) { slot = i; break; }
         if (k < 0 && free_slot < 0) free_slot = i;
     }
+    arbiter_update_found(S, L, e, key, ta, ba, tb, bb, ua, ub, info, slot, free_slot);
+}
+MG_DEV void arbiter_update_found(const MGState &S, const mg_library *L, int e, int key, int ta, int ba, int tb,
+                                 int bb, double ua, double ub, const Collision &info, int slot, int free_slot) {
     if (slot < 0) {
         if (free_slot < 0) { S.overflow[e] |= 1; return; }
         slot = free_slot;
@@ -1648,19 +1656,20 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
                 c.hash[k] = rl_u64(info.hash[k], src);
             }
             const int si = __builtin_amdgcn_readlane(i, src), sj = __builtin_amdgcn_readlane(j, src);
+            const int key = sj < 0 ? si * 128 + 100 + (-1 - sj) : si * 128 + sj;
+            // the arbiter slot search across the wavefront (the serial search's first match / first empty slot;
+            // lane 0's update of the previous hit is ordered before these reads by the wave's in-order LDS)
+            const int ak = lane < S.arb_cap ? AT(S.akey, lane) : 0;
+            const uint64_t hm = __ballot(lane < S.arb_cap && ak == key), fm = __ballot(lane < S.arb_cap && ak < 0);
+            const int fslot = hm ? __ffsll((long long)hm) - 1 : -1, ffree = fm ? __ffsll((long long)fm) - 1 : -1;
             if (lane == 0) {
-                ShapeW A, B; // arbiter_update reads the shapes' types and bodies only
-                A.type = AT(S.spoly, si) < 0 ? WS_CIRCLE : WS_POLY;
-                A.body = AT(S.sbody, si);
+                // arbiter_update reads the shapes' types and bodies only
+                const int ta = AT(S.spoly, si) < 0 ? WS_CIRCLE : WS_POLY, ba = AT(S.sbody, si);
+                int tb, bb;
                 double ub;
-                int key;
-                if (sj < 0) {
-                    B.type = WS_SEGMENT; B.body = -1; ub = 0.8; key = si * 128 + 100 + (-1 - sj);
-                } else {
-                    B.type = AT(S.spoly, sj) < 0 ? WS_CIRCLE : WS_POLY; B.body = AT(S.sbody, sj);
-                    ub = AT(S.su, sj); key = si * 128 + sj;
-                }
-                arbiter_update(S, L, e, key, A, B, AT(S.su, si), ub, c);
+                if (sj < 0) { tb = WS_SEGMENT; bb = -1; ub = 0.8; }
+                else { tb = AT(S.spoly, sj) < 0 ? WS_CIRCLE : WS_POLY; bb = AT(S.sbody, sj); ub = AT(S.su, sj); }
+                arbiter_update_found(S, L, e, key, ta, ba, tb, bb, AT(S.su, si), ub, c, fslot, ffree);
             }
         }
         MG_PP(P, 9);
