@@ -936,6 +936,13 @@ MG_DEV void static_solve(const MGState &S, int e, double dt, double dt_coef, int
 #ifndef MG_COOP_COMPACT
 #define MG_COOP_COMPACT 1
 #endif
+#ifdef MG_EXP_SAT2
+MG_DEV bool surely_apart_x2(const MGState &S, const mg_library *L, int e, int i, int j) {
+    int i2 = i;
+    asm volatile("" : "+v"(i2));   // an opaque copy: the compiler cannot merge the two tests
+    return surely_apart(S, L, e, i2, j);
+}
+#endif
 // ---- cpSpaceStep -----------------------------------------------------------
 // one lane per env on the HBM state (variant 0, scenes beyond the LDS forms' caps): runtime constraint lists
 MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, MGProf &P) {
@@ -1607,6 +1614,9 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
                     const int gi = AT(S.sgroup, i), gj = AT(S.sgroup, j);
                     hit = al <= AT(S.sbbr, j) && AT(S.sbbl, j) <= ar && ab <= AT(S.sbbt, j) && AT(S.sbbb, j) <= at &&
                           AT(S.sbody, j) != AT(S.sbody, i) && !(gi != 0 && gi == gj) && !((gi | gj) & MG_GROUP_OFF) &&
+#ifdef MG_EXP_SAT2          // timing experiments only: the separating-axis test twice (idempotent)
+                          !surely_apart_x2(S, L, e, i, j) &&
+#endif
                           !surely_apart(S, L, e, i, j);
                 }
             }
