@@ -79,6 +79,12 @@ int mg_render_full(mg_sim *sim, uint8_t *out_dev, void *stream);
 /* parity dumps: per env per body slot (px, py, angle, vx, vy, w): device f64[N,16,6];
  * counts: device i32[N,4] = (bodies, shapes, constraints, active arbiters) */
 int mg_get_bodies(mg_sim *sim, double *out_dev, int32_t *counts_dev, void *stream);
+/* parity dumps of the contact solver's state (cpArbiter / cpContact): the solved
+ * arbiters of every env in active order, out_dev f64[N,48,28] = (slot, state, count, body a, body b, n.x, n.y,
+ * friction u, then per contact r1.x, r1.y, r2.x, r2.y, jnAcc, jtAcc, nMass, tMass, bias, jBias), hash_dev
+ * u64[N,48,2] = the contacts' feature hashes; rows past the env's active count are zero.  Test hook of the
+ * parity suite (the reference has no such call: pymunk exposes the same data as Arbiter.contact_point_set) */
+int mg_get_arbiters(mg_sim *sim, double *out_dev, uint64_t *hash_dev, void *stream);
 /* set body `body` of env `env` to (x, y, angle) like pymunk's Body.position / Body.angle setters
  * (geom.py:362-384 pm_shift_bodies applies them); for parity tests that place blocks before a step */
 int mg_set_body_pose(mg_sim *sim, int env, int body, double x, double y, double angle, void *stream);

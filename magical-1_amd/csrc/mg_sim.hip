@@ -92,6 +92,32 @@ __global__ void __launch_bounds__(64) bodies_kernel(MGState S, double *out, int3
     }
 }
 
+// the solved arbiters of every env in active order (oracle/env.c oenv_get_arbiters has the same layout)
+#define MG_ARB_DUMP 28
+__global__ void __launch_bounds__(64) arbiters_kernel(MGState S, double *out, uint64_t *hash) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= S.n_envs) return;
+    const int na = S.nactive[e];
+    for (int i = 0; i < MG_MAX_ARB; i++) {
+        double *o = out + ((size_t)e * MG_MAX_ARB + i) * MG_ARB_DUMP;
+        uint64_t *h = hash + ((size_t)e * MG_MAX_ARB + i) * 2;
+        for (int k = 0; k < MG_ARB_DUMP; k++) o[k] = 0.0;
+        h[0] = h[1] = 0;
+        if (i >= na) continue;
+        const int slot = AT(S.active, i), cnt = AT(S.acount, slot);
+        o[0] = slot; o[1] = AT(S.astate, slot); o[2] = cnt; o[3] = AT(S.asa, slot); o[4] = AT(S.asb, slot);
+        o[5] = AT(S.anx, slot); o[6] = AT(S.any, slot); o[7] = AT(S.au, slot);
+        for (int k = 0; k < cnt && k < 2; k++) {
+            double *q = o + 8 + 10 * k;
+            q[0] = ACON(k, AC_R1X, slot); q[1] = ACON(k, AC_R1Y, slot); q[2] = ACON(k, AC_R2X, slot);
+            q[3] = ACON(k, AC_R2Y, slot); q[4] = ACON(k, AC_JN, slot); q[5] = ACON(k, AC_JT, slot);
+            q[6] = ACON(k, AC_NMASS, slot); q[7] = ACON(k, AC_TMASS, slot); q[8] = ACON(k, AC_BIAS, slot);
+            q[9] = ACON(k, AC_JB, slot);
+            h[k] = AHASH(k, slot);
+        }
+    }
+}
+
 __global__ void __launch_bounds__(64) errors_kernel(MGState S, int32_t *out) {
     int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= S.n_envs) return;
@@ -652,6 +678,14 @@ int mg_get_bodies(mg_sim *s, double *out, int32_t *counts, void *stream) {
     if (!s || !out) return set_err(-22, "mg_get_bodies: null argument");
     HIPC(hipSetDevice(s->device));
     hipLaunchKernelGGL(bodies_kernel, dim3(grid64(s)), dim3(64), 0, as_stream(stream), s->S, out, counts);
+    HIPC(hipGetLastError());
+    return 0;
+}
+
+int mg_get_arbiters(mg_sim *s, double *out, uint64_t *hash, void *stream) {
+    if (!s || !out || !hash) return set_err(-22, "mg_get_arbiters: null argument");
+    HIPC(hipSetDevice(s->device));
+    hipLaunchKernelGGL(arbiters_kernel, dim3(grid64(s)), dim3(64), 0, as_stream(stream), s->S, out, hash);
     HIPC(hipGetLastError());
     return 0;
 }

@@ -283,6 +283,15 @@ class VecMagicalEnv:
                                             ctypes.c_void_p(counts.data_ptr()), self._stream()))
         return out, counts
 
+    def arbiters(self):
+        """solved arbiters per env in active order: f64 [N, 48, 28] and contact hashes u64 [N, 48, 2]
+        (mg_get_arbiters; the active count is bodies()[1][:, 3])"""
+        out = torch.empty((self.num_envs, 48, 28), dtype=torch.float64, device=self.device)
+        hs = torch.empty((self.num_envs, 48, 2), dtype=torch.uint64, device=self.device)
+        native.check(self.lib.mg_get_arbiters(self.handle, ctypes.c_void_p(out.data_ptr()),
+                                              ctypes.c_void_p(hs.data_ptr()), self._stream()))
+        return out, hs
+
     def set_body_pose(self, env, body, x, y, angle):
         """Place body `body` of env `env` (Body.position / Body.angle setters; parity tests)."""
         native.check(self.lib.mg_set_body_pose(self.handle, int(env), int(body), float(x), float(y), float(angle),

@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(HERE, "libmagical_sim_prof.so" if os.environ.get("MAGICA
 if os.environ.get("MAGICAL_AMD_EXP_LIB"):   # A/B kernel experiments (tools/gpu_ab.sh): an in-tree build variant
     LIB_PATH = os.path.join(HERE, "libmagical_sim_%s.so" % os.path.basename(os.environ["MAGICAL_AMD_EXP_LIB"]))
 
-EXPORTS = ["mg_create", "mg_bind_outputs", "mg_reset", "mg_step", "mg_render_full", "mg_get_bodies",
+EXPORTS = ["mg_create", "mg_bind_outputs", "mg_reset", "mg_step", "mg_render_full", "mg_get_bodies", "mg_get_arbiters",
            "mg_set_body_pose", "mg_get_errors", "mg_seed", "mg_random_actions", "mg_num_envs", "mg_enable_timing", "mg_read_timing",
            "mg_set_episode_steps", "mg_selftest_sincos", "mg_replay_lores", "mg_restack", "mg_restack_window", "mg_bind_window",
            "mg_window_start", "mg_destroy", "mg_last_error"]
@@ -56,6 +56,8 @@ def load():
     lib.mg_render_full.argtypes = [vp, vp, vp]
     lib.mg_get_bodies.argtypes = [vp, vp, vp, vp]
     lib.mg_get_errors.argtypes = [vp, vp, vp]
+    if hasattr(lib, "mg_get_arbiters"):
+        lib.mg_get_arbiters.argtypes = [vp, vp, vp, vp]
     lib.mg_set_body_pose.argtypes = [vp, i32, i32, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
     lib.mg_seed.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
     lib.mg_random_actions.argtypes = [vp, vp, u64, u64, vp]

@@ -138,6 +138,31 @@ int oenv_get_bodies(const OEnv *e, double *out, int max_bodies) {
 
 int oenv_num_arbiters(const OEnv *e) { return e->space.nactive; }
 
+/* the solved arbiters in active order (cpSpace arbiters list), as mg_get_arbiters dumps them:
+ * out[i][28] = [slot, state, count, body a, body b, n.x, n.y, u, 2 x (r1.x, r1.y, r2.x, r2.y, jnAcc, jtAcc,
+ * nMass, tMass, bias, jBias)], hash[i][2]; returns the number of arbiters written */
+int oenv_get_arbiters(const OEnv *e, double *out, uint64_t *hash, int max_arbs) {
+    int n = e->space.nactive < max_arbs ? e->space.nactive : max_arbs;
+    for (int i = 0; i < n; i++) {
+        const int slot = e->space.active[i];
+        const OArbiter *A = &e->space.arbs[slot];
+        double *o = out + 28 * i;
+        for (int k = 0; k < 28; k++) o[k] = 0.0;
+        o[0] = slot; o[1] = A->state; o[2] = A->count;
+        o[3] = e->space.shapes[A->sa].body; o[4] = e->space.shapes[A->sb].body;
+        o[5] = A->n.x; o[6] = A->n.y; o[7] = A->u;
+        hash[2 * i] = hash[2 * i + 1] = 0;
+        for (int k = 0; k < A->count; k++) {
+            const OContact *c = &A->con[k];
+            double *q = o + 8 + 10 * k;
+            q[0] = c->r1.x; q[1] = c->r1.y; q[2] = c->r2.x; q[3] = c->r2.y; q[4] = c->jnAcc; q[5] = c->jtAcc;
+            q[6] = c->nMass; q[7] = c->tMass; q[8] = c->bias; q[9] = c->jBias;
+            hash[2 * i + k] = c->hash;
+        }
+    }
+    return n;
+}
+
 /* pymunk Body.angle / Body.position setters on body b (as geom.pm_shift_bodies applies them),
  * shapes reindexed: parity tests move blocks to chosen poses before a step */
 void oenv_get_target(const OEnv *e, double out[4]) {

@@ -121,5 +121,6 @@ int ophys_collide(OSpace *s, int a, int b, OCollision *out, int *swapped);
 int ophys_shape_query_any(OSpace *s, int sh);
 int ophys_shape_query_any_ign(OSpace *s, int sh, const uint8_t *ign);
 double ophys_poly_point_query(const OShape *sh, vec2 p);
+extern long ophys_epa_runs; /* EPA runs so far (tests) */
 
 #endif

@@ -98,6 +98,7 @@ void oenv_render_full(OEnv *e, uint8_t *allo, uint8_t *ego);
 /* per dynamic/kinematic body: px, py, a, vx, vy, w  (returns body count) */
 int oenv_get_bodies(const OEnv *e, double *out, int max_bodies);
 int oenv_num_arbiters(const OEnv *e);
+int oenv_get_arbiters(const OEnv *e, double *out, uint64_t *hash, int max_arbs);
 void oenv_set_body_pose(OEnv *e, int body, double x, double y, double angle);
 /* PickAndPlace observation extras: (target_type, target_colour, target_position x, y) */
 void oenv_get_target(const OEnv *e, double out[4]);

@@ -588,9 +588,13 @@ static OClosest closest_points_new(MinkowskiPoint v0, MinkowskiPoint v1) {
 #define MAX_GJK_ITERATIONS 30
 #define MAX_EPA_ITERATIONS 30
 
+/* number of EPA runs so far (the known-answer tests check which path a configuration takes) */
+long ophys_epa_runs = 0;
+
 static OClosest epa(const SupportCtx *ctx, MinkowskiPoint v0, MinkowskiPoint v1, MinkowskiPoint v2_) {
     MinkowskiPoint hull[64], hull2[64];
     int count = 3;
+    ophys_epa_runs++;
     hull[0] = v0; hull[1] = v1; hull[2] = v2_;
     for (int iteration = 1;; iteration++) {
         int mini = 0;

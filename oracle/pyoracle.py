@@ -46,6 +46,7 @@ def lib():
         L.oenv_render_full.argtypes = [vp, vp, vp]
         L.oenv_get_bodies.restype = i; L.oenv_get_bodies.argtypes = [vp, vp, i]
         L.oenv_num_arbiters.restype = i; L.oenv_num_arbiters.argtypes = [vp]
+        L.oenv_get_arbiters.restype = i; L.oenv_get_arbiters.argtypes = [vp, vp, vp, i]
         L.oenv_placement_retries.restype = i; L.oenv_placement_retries.argtypes = [vp]
         L.oenv_set_max_tries.argtypes = [vp, i]
         L.oenv_get_entities.restype = i; L.oenv_get_entities.argtypes = [vp, vp, vp, vp, vp]
@@ -188,6 +189,14 @@ class OracleEnv:
 
     def num_arbiters(self):
         return self.L.oenv_num_arbiters(self.h)
+
+    def arbiters(self):
+        """the solved arbiters in active order: f64 [n, 28] (slot, state, count, body a, body b, n.x, n.y, u,
+        2 x (r1, r2, jnAcc, jtAcc, nMass, tMass, bias, jBias)) and u64 [n, 2] contact hashes (mg_get_arbiters)"""
+        out = np.zeros((64, 28))
+        hs = np.zeros((64, 2), dtype=np.uint64)
+        n = self.L.oenv_get_arbiters(self.h, ptr(out), ptr(hs), 64)
+        return out[:n].copy(), hs[:n].copy()
 
     def entity_poses(self):
         """per entity after the arena, in add order: (x, y, angle) of each of its bodies (the goal: its static
