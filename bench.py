@@ -54,6 +54,41 @@ def kernel_survey_bytes(kernel, preproc):
     return survey_bytes(preproc) if kernel == "render_kernel" else STATE_BYTES
 
 
+AC_NUM = 10                 # contact fields per arbiter contact (csrc/mg_state.h)
+
+
+def step_state_bytes(form, caps, live_arbiters):
+    """Bytes per env-step the step kernel's HBM state transfer moves by its design (csrc/mg_stepk.h): the
+    substeps run on an LDS copy of the env's state, loaded once (xfer_state_quad, or the cooperative form's
+    xfer_state, `in`) and written back once (xfer_state `out`), every [slot][N] row up to the form's slot caps
+    (bodies nb, shapes ns, constraints nc, arbiter slots na); arbiter slots carry contact data only while live.
+      in:  bodies 12 x nb f64 (p, v, angle, w, bias velocities, rotation cache) + 1/m, 1/I (2 x nb f64);
+           constraint slots MAXF..JACC2 and parameters 8-11 (9 x nc f64); arbiter keys (na i32), per live slot
+           n, u (3 f64), stamp (u32), state / count / bodies (4 i8), 2 contacts x 10 f64, 2 hashes (u64), its
+           active-list entry (i8); nactive, stamp, overflow (3 x 4), curr_dt, target_speed, rel_turn,
+           target_finger (4 x f64), nbodies / nshapes / ncons / robot_body0 / robot_cons0 (5 x i32); per shape
+           radius, friction (2 f64), group, hashid (2 i16), body, poly (2 i8); the cooperative form also its
+           runtime constraint list (3 x nc i8);
+      out: bodies 12 x nb f64, warm-start impulses JACC / JACC2 (2 x nc f64), arbiter keys and live slots as
+           in, nactive, curr_dt, stamp, overflow;
+      io:  action (u8), episode_steps (r/w i32), reward (f32), done (u8), eval_score (f64), reset mask (u8).
+    The fused / shadow resets and the library (L2-resident, shared by every env) are not counted."""
+    nb, ns, nc, na = caps
+    live = float(live_arbiters)
+    slot = 3 * 8 + 4 + 4 + 2 * AC_NUM * 8 + 2 * 8 + 1
+    arbs = na * 4 + live * slot + 4
+    rd = 14 * nb * 8 + 9 * nc * 8 + arbs + 3 * 4 + 4 * 8 + 5 * 4 + ns * (2 * 8 + 2 * 2 + 2) + (3 * nc if form == 4 else 0)
+    wr = 12 * nb * 8 + 2 * nc * 8 + arbs + 8 + 4 + 4
+    io = 1 + 2 * 4 + 4 + 1 + 8 + 1
+    return int(round(rd + wr + io))
+
+
+def env_overrides():
+    """Every MG_* / MAGICAL_AMD_* variable set in this process's environment (they select kernel forms, block
+    sizes, reset paths or a library variant at mg_create): recorded on the bench line"""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith(("MG_", "MAGICAL_AMD_"))}
+
+
 def obs_bytes(preproc):
     return {"LoRes4E": 165888, "LoRes4A": 165888, "LoRes3EA": 165888, "LoResCHW4E": 165888, "LoResCHW4A": 165888,
             "LoResStack": 221184}.get(preproc, 2 * 384 * 384 * 3)
@@ -209,21 +244,21 @@ def launch_ranks(n):
     return subprocess.call(cmd, env=dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1")))
 
 
-def kernel_record(name, ms, preproc, n, pmc, frames_only=False, window=False):
-    """One kernel's roofline figures over its HIP-event average duration (ms per launch, one launch per step):
+def kernel_record(name, ms, preproc, n, pmc, frames_only=False, window=False, step_bytes=None):
+    """One kernel's roofline figures over its average duration (ms per launch, one launch per step):
     * achieved / hbm_frac: SURVEY 8(d) bytes of the env-steps the launch completes (survey_bytes x n);
-    * traffic_ratio: PMC HBM bytes per launch (committed rocprofv3 FETCH/WRITE passes of the same workload
-      and env count) over the kernel's own 8(d) share x n (render: obs + state, step: state);
     * kernel_bytes_*: the bytes this kernel must move by its design (render: obs + the frame ring's reads
-      and writes; step: state) -- the ring-inclusive figure of earlier rounds."""
+      and writes; step: its state transfer, step_state_bytes, when given -- else the 8(d) nominal 2 KB);
+    * traffic_ratio: PMC HBM bytes per launch (committed rocprofv3 FETCH/WRITE passes of the same workload
+      and env count) over the render kernel's 8(d) share x n (obs + state), the step kernel's design bytes x n."""
     if ms is None or ms <= 0:
         return None
     sb = survey_bytes(preproc)
     ach = sb * n / (ms * 1e-3) / 1e9
-    kb = render_bytes(preproc, frames_only, window) if name == "render_kernel" else STATE_BYTES
+    kb = render_bytes(preproc, frames_only, window) if name == "render_kernel" else (step_bytes or STATE_BYTES)
     kach = kb * n / (ms * 1e-3) / 1e9
     traffic = pmc and pmc.get("bytes_per_launch")
-    share = kernel_survey_bytes(name, preproc)
+    share = kernel_survey_bytes(name, preproc) if name == "render_kernel" else kb
     return {"ms": round(ms, 4), "bytes_per_env_step": sb, "achieved_gbs": round(ach, 2),
             "hbm_frac": round(ach / HBM_PEAK_GBS, 5),
             "traffic_bytes_per_launch": traffic,
@@ -385,17 +420,24 @@ def main():
     t_step_ms, t_render_ms, n_timed = tm[0] / args.steps, tm[1] / args.steps, int(tm[2])
     t_reset_ms = tm[3] / args.steps
     units = n / chunks   # envs one kernel launch completes (on average over the chunks)
-    # chunked runs: the timed launches overlap the other chunk's kernels, so their HIP-event times are
-    # co-running figures.  The roofline's per-kernel times come from an isolated pass after the timed region:
-    # chunk 0 stepped alone (its step, reset and render kernels back to back on one stream, nothing beside
-    # them), args.iso_steps steps of the same env count per launch.
+    errors = int((vec.errors() != 0).sum().item())   # the timed run's (before the isolated pass below)
+    sim0 = vec.sims[0] if chunks > 1 else vec
+    form, blk, caps = sim0.step_form()
+    live = float(sim0.bodies()[1][:, 3].double().mean().item())   # active arbiters per env after the timed run
+    step_bytes = step_state_bytes(form, caps, live)
+    # The timed launches' HIP-event times are co-running figures: chunked runs overlap the other chunk's kernels,
+    # and the many-block scenes' next-layout shadow (reset_kernel on the simulator's side stream) co-runs with
+    # the step and render kernels.  The roofline's per-kernel times come from an isolated pass after the timed
+    # region: one simulator (chunk 0 of a pool) stepped alone, the device synchronised before every step, so its
+    # step kernel has nothing beside it (the shadow's launch follows the step kernel and overlaps the render,
+    # as in every step), args.iso_steps steps of the same env count per launch.
     iso = None
-    if chunks > 1 and args.iso_steps > 0:
-        sim0 = vec.sims[0]
+    if args.iso_steps > 0:
         native.check(lib.mg_enable_timing(sim0.handle, args.iso_steps))
         a0 = torch.empty(sim0.num_envs, dtype=torch.uint8, device=device)
         for s in range(args.iso_steps):
             sim0.random_actions(10 ** 6 + s, out=a0)
+            torch.cuda.synchronize(device)
             sim0.step(a0)
         torch.cuda.synchronize(device)
         ti = (ctypes.c_double * 4)()
@@ -408,7 +450,6 @@ def main():
         """The committed PMC record of this workload at this many envs per launch (the passes run the bench's
         own chunking; rocprofv3 counts each dispatch on its own)."""
         return load_pmc(kernel, args.env, n, units)
-    errors = int((vec.errors() != 0).sum().item())
     ranks_seen = world
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -429,9 +470,13 @@ def main():
         kernels = {
             "render_kernel": kernel_record("render_kernel", k_render, spec.preproc, units,
                                            pmc_for("render_kernel"), frames_only, stacks_window),
-            "step_kernel": kernel_record("step_kernel", k_step, spec.preproc, units, pmc_for("step_kernel")),
+            "step_kernel": kernel_record("step_kernel", k_step, spec.preproc, units, pmc_for("step_kernel"),
+                                         step_bytes=step_bytes),
             "reset_kernel": {"ms": round(k_reset, 4)},
-            "timing": "isolated (chunk 0 alone after the timed region)" if iso else "timed launches (one stream)",
+            "timing": ("isolated (after the timed region: " + ("chunk 0" if chunks > 1 else "the simulator") +
+                       " stepped alone, device synchronised before each step)") if iso else "timed launches (one stream)",
+            "step_form": {"form": form, "envs_per_workgroup": blk, "caps_bodies_shapes_constraints_arbiters": caps,
+                          "live_arbiters_per_env": round(live, 3), "state_bytes_per_env_step": step_bytes},
         }
         dom = "render_kernel" if k_render >= k_step else "step_kernel"
         dk = kernels[dom]
@@ -459,6 +504,8 @@ def main():
             "config": {"workload": args.env, "envs_per_gpu": n, "episode_steps": spec.max_episode_steps,
                        "physics_substeps": 10, "solver_iterations": 10, "render": "2 x 384^2 -> 96^2",
                        "phase_spread": phase_spread,
+                       "step_form": f"{form}/{blk}",
+                       "env_overrides": env_overrides(),
                        "pipeline_chunks": chunks,
                        "frame_stacks": ("strided views of channel-planar window rings (mg_bind_window)"
                                         if stacks_window else "materialised [N, 96, 96, 12]" if not gather else

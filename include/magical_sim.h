@@ -100,6 +100,10 @@ int mg_seed(mg_sim *sim, const uint32_t *seeds_host);
 /* device-side uniform random actions for throughput runs (Philox 4x32-10, key, counter = (step, env)) */
 int mg_random_actions(mg_sim *sim, uint8_t *actions_dev, uint64_t key, uint64_t step, void *stream);
 int mg_num_envs(const mg_sim *sim);
+/* the step kernel this handle launches (diagnostics for bench.py's byte model): out i32[6] = (form: 0 HBM state,
+ * 4 cooperative, 5 / 6 robot-scene quad forms; envs per workgroup; the per-env slot caps its HBM <-> LDS transfer
+ * moves: bodies, shapes, constraints, arbiter slots) */
+int mg_step_form(const mg_sim *sim, int32_t *out);
 /* self-test of the device's correctly rounded sin/cos (the physics and render transforms use it):
  * device f64 x[n] -> sin, cos */
 int mg_selftest_sincos(const double *x_dev, double *sin_dev, double *cos_dev, int n, void *stream);

@@ -15,6 +15,7 @@
 #define MG_MAX_SHAPES 64
 #define MG_MAX_CONS 32
 #define MG_MAX_ARB 48
+#define MG_ITERATIONS 10   // Space.iterations (base_env.py:208): solver sweeps per substep
 #define MG_MAX_ENTS 14
 #define MG_MAX_PVERTS 8
 #define MG_MAX_LIB_POLYS 32

@@ -156,10 +156,6 @@ __device__ __noinline__ void mg_sincos_slow(double rh, double rl, int q, double 
 
 // correctly rounded (cos x, sin x)
 MG_DEV void mg_sincos(double x, double &s, double &c) {
-#ifdef MG_EXP_FAST_SINCOS   // timing experiments only (tools/build_unit_variant.sh): NOT correctly rounded
-    sincos(x, &s, &c);
-    return;
-#endif
     if (fabs(x) < 7.450580596923828e-09) { s = x; c = 1.0; return; }
     int q; dd_t r;
     mg_reduce_pio2(x, q, r);

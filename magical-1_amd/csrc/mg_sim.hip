@@ -639,6 +639,18 @@ int mg_restack_window(const uint8_t *recv, int32_t world, int32_t n, int64_t ran
 
 int mg_bind_window(mg_sim *s, uint8_t *ring_allo, uint8_t *ring_ego, int32_t K) {
     if (!s) return set_err(-22, "mg_bind_window: null sim");
+    // outputs bound while rings were on may leave the stacked outputs null (mg_bind_outputs): turning the rings
+    // off, or changing which views have one, would then make the next render write its stacks through null
+    // pointers -- refuse until outputs with the stacks are bound
+    if (s->bound && !s->out.frames_only) {
+        const int pp = s->preproc;
+        const bool lost = pp == MG_PREPROC_LORESSTACK ? ((!ring_allo && !s->out.obs_allo) || (!ring_ego && !s->out.obs_ego))
+                        : pp == MG_PREPROC_LORES4E    ? (!ring_ego && !s->out.obs_past)
+                        : pp == MG_PREPROC_LORES4A    ? (!ring_allo && !s->out.obs_past) : false;
+        if (lost)
+            return set_err(-22, "mg_bind_window: a stacked view would have neither a ring nor an output buffer (the "
+                                "bound outputs' stacks are null); bind outputs with the stacks (mg_bind_outputs) first");
+    }
     if (!ring_allo && !ring_ego) { s->wring[0] = s->wring[1] = nullptr; s->wK = 0; return 0; }
     if (K < 4 || K > 64) return set_err(-22, "mg_bind_window: K must be in [4, 64]");
     const int pp = s->preproc;
@@ -733,6 +745,20 @@ int mg_random_actions(mg_sim *s, uint8_t *actions, uint64_t key, uint64_t step, 
 }
 
 int mg_num_envs(const mg_sim *s) { return s ? s->S.n_envs : -22; }
+
+int mg_step_form(const mg_sim *s, int32_t *out) {
+    if (!s || !out) return set_err(-22, "mg_step_form: null argument");
+    out[0] = s->step_variant; out[1] = s->step_blk;
+    out[2] = s->caps.nb; out[3] = s->caps.ns; out[4] = s->caps.nc; out[5] = s->caps.na;
+    if (s->step_variant == 5 || s->step_variant == 6) {   // the quad forms' compile-time caps (mg_stepk.h)
+        const int q[2][4] = {{6, 5, 10, 20}, {7, 6, 12, 32}};
+        for (int k = 0; k < 4; k++) out[2 + k] = q[s->step_variant - 5][k];
+    } else if (s->step_variant != 0) {
+        const StepCaps c = step_variant_caps(s->step_variant);
+        out[2] = c.nb; out[3] = c.ns; out[4] = c.nc; out[5] = c.na;
+    }
+    return 0;
+}
 
 __global__ void __launch_bounds__(64) set_episode_steps_kernel(MGState S, const int32_t *steps) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;

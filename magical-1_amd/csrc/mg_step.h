@@ -681,7 +681,6 @@ MG_DEV void harb_cached_k(RegBodies<NB> &R, const MGState &S, int e, int slot, d
 template <int NB>
 MG_DEV void harb_cached_row(RegBodies<NB> &R, const MGState &S, int e, int slot, double dt_coef) {
     if (AT(S.astate, slot) == ARB_FIRST) return;
-#ifndef MG_EXP_HARB_SELECT
     const int sa = AT(S.asa, slot), sb = AT(S.asb, slot);
     if (sa == 0 && sb < 0) { harb_cached_k<NB, 0, -1>(R, S, e, slot, dt_coef); return; }
     if (sa < 0 && sb == 4) { harb_cached_k<NB, -1, 4>(R, S, e, slot, dt_coef); return; }
@@ -692,7 +691,6 @@ MG_DEV void harb_cached_row(RegBodies<NB> &R, const MGState &S, int e, int slot,
         if (sa == 4 && sb == 6) { harb_cached_k<NB, 4, 6>(R, S, e, slot, dt_coef); return; }
         if (sa == 5 && sb == 6) { harb_cached_k<NB, 5, 6>(R, S, e, slot, dt_coef); return; }
     }
-#endif
     harb_cached(R, S, e, slot, dt_coef);
 }
 
@@ -701,7 +699,6 @@ MG_DEV void harb_cached_row(RegBodies<NB> &R, const MGState &S, int e, int slot,
 // or the block (shape_body_slot) -- to harb_apply_k; any other pair takes the select form
 template <int NB>
 MG_DEV void harb_row(RegBodies<NB> &R, const MGState &S, int e, int slot) {
-#ifndef MG_EXP_HARB_SELECT  // timing experiments only: every arbiter row through the one-hot selects
     const int sa = AT(S.asa, slot), sb = AT(S.asb, slot);
     if (sa == 0 && sb < 0) { harb_apply_k<NB, 0, -1>(R, S, e, slot); return; }
     if (sa < 0 && sb == 4) { harb_apply_k<NB, -1, 4>(R, S, e, slot); return; }
@@ -712,7 +709,6 @@ MG_DEV void harb_row(RegBodies<NB> &R, const MGState &S, int e, int slot) {
         if (sa == 4 && sb == 6) { harb_apply_k<NB, 4, 6>(R, S, e, slot); return; }
         if (sa == 5 && sb == 6) { harb_apply_k<NB, 5, 6>(R, S, e, slot); return; }
     }
-#endif
     harb_apply(R, S, e, slot);
 }
 
@@ -874,18 +870,6 @@ MG_DEV void static_solve(const MGState &S, int e, double dt, double dt_coef, int
     for (int i = 0; i < nact; i++) harb_cached_row(R, S, e, AT(S.active, i), dt_coef);
     rstatic_cached<NCS>(R, q, dt_coef);
     MG_PP(P, 5);
-#ifndef MG_EXP_ITERS        // timing experiments only (tools/build_unit_variant.sh)
-#define MG_EXP_ITERS 10
-#endif
-#ifdef MG_EXP_NOARBIT       // timing experiments only: no arbiter rows in the iterations
-    nact = 0;
-#endif
-#ifdef MG_EXP_ARBSTAT       // statistics experiments only: substeps with live arbiters, counted in bits 12+
-    if (nact > 0) S.overflow[e] += 1 << 12;
-#endif
-#ifdef MG_ISA_MARK          // ISA reading only: comment markers around the iteration loop
-    asm volatile("; MG_ITER_BEGIN");
-#endif
     // the first NARB arbiters in registers when their pairs are compile-time ones (the rest through LDS)
     RegArb ra[NARB > 0 ? NARB : 1];
     int nreg = 0;
@@ -903,27 +887,15 @@ MG_DEV void static_solve(const MGState &S, int e, double dt, double dt_coef, int
         }
     }
 #pragma unroll 1
-    for (int it = 0; it < MG_EXP_ITERS; it++) {
+    for (int it = 0; it < MG_ITERATIONS; it++) {
         if constexpr (NARB > 0) {
 #pragma unroll
             for (int i = 0; i < NARB; i++)
                 if (i < nreg) rarb_row(R, ra[i]);
         }
         for (int i = nreg; i < nact; i++) harb_row(R, S, e, AT(S.active, i));
-#ifdef MG_ISA_MARK
-        asm volatile("; MG_ROWS_BEGIN");
-#endif
         rstatic_apply<NCS>(R, q);
-#ifdef MG_EXP_ROWS2         // timing experiments only: the constraint rows twice per iteration
-        rstatic_apply<NCS>(R, q);
-#endif
-#ifdef MG_ISA_MARK
-        asm volatile("; MG_ROWS_END");
-#endif
     }
-#ifdef MG_ISA_MARK
-    asm volatile("; MG_ITER_END");
-#endif
     if constexpr (NARB > 0) {
 #pragma unroll
         for (int i = 0; i < NARB; i++)
@@ -935,13 +907,6 @@ MG_DEV void static_solve(const MGState &S, int e, double dt, double dt_coef, int
 
 #ifndef MG_COOP_COMPACT
 #define MG_COOP_COMPACT 1
-#endif
-#ifdef MG_EXP_SAT2
-MG_DEV bool surely_apart_x2(const MGState &S, const mg_library *L, int e, int i, int j) {
-    int i2 = i;
-    asm volatile("" : "+v"(i2));   // an opaque copy: the compiler cannot merge the two tests
-    return surely_apart(S, L, e, i2, j);
-}
 #endif
 // ---- cpSpaceStep -----------------------------------------------------------
 // one lane per env on the HBM state (variant 0, scenes beyond the LDS forms' caps): runtime constraint lists
@@ -965,9 +930,6 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
     MG_PP(P, 1);
     // broadphase + narrowphase, canonical order
     ShapeW A, W, B;   // narrowphase operands (per-lane scratch)
-#ifdef MG_EXP_NO_NARROW     // timing experiments only (tools/build_unit_variant.sh): no collisions at all
-    ns = 0;
-#endif
     for (int i = 0; i < ns; i++) {
         // BB tests on the cached BBs; the world-space shape is built only for pairs that pass
         const double al = AT(S.sbbl, i), ab = AT(S.sbbb, i), ar = AT(S.sbbr, i), at = AT(S.sbbt, i);
@@ -1017,7 +979,7 @@ MG_DEV void space_step(const MGState &S, const mg_library *L, int e, double dt, 
     for (int i = 0; i < nact; i++) arbiter_cached(S, e, AT(S.active, i), dt_coef);
     for (int c = 0; c < nc; c++) cons_cached(S, e, c, dt_coef);
     MG_PP(P, 5);
-    for (int it = 0; it < 10; it++) {
+    for (int it = 0; it < MG_ITERATIONS; it++) {
         for (int i = 0; i < nact; i++) arbiter_apply(S, e, AT(S.active, i));
         for (int c = 0; c < nc; c++) cons_apply(S, e, c, dt);
     }
@@ -1614,9 +1576,6 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
                     const int gi = AT(S.sgroup, i), gj = AT(S.sgroup, j);
                     hit = al <= AT(S.sbbr, j) && AT(S.sbbl, j) <= ar && ab <= AT(S.sbbt, j) && AT(S.sbbb, j) <= at &&
                           AT(S.sbody, j) != AT(S.sbody, i) && !(gi != 0 && gi == gj) && !((gi | gj) & MG_GROUP_OFF) &&
-#ifdef MG_EXP_SAT2          // timing experiments only: the separating-axis test twice (idempotent)
-                          !surely_apart_x2(S, L, e, i, j) &&
-#endif
                           !surely_apart(S, L, e, i, j);
                 }
             }
@@ -1795,10 +1754,6 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
     const double dt_coef = (prev_dt == 0.0 ? 0.0 : dt / prev_dt);
     const int unact = ufirst(nact), unc = ufirst(nc);
     const GroundRows &G = Q.G;
-#ifndef MG_EXP_COOP_ITERS   // timing experiments only (tools/build_unit_variant.sh)
-#define MG_EXP_COOP_ITERS 10
-#endif
-#ifndef MG_EXP_COOP_NORR   // timing experiments only: the lane-select robot rows below
     const int rb0 = Q.rb0, rc0 = Q.rc0;
     if (Q.rstatic) {
         RobotV V;
@@ -1823,25 +1778,13 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
         rrows_cached(V, S, e, rc0, dt_coef);
         MG_PP(P, 5);
 #pragma unroll 1
-        for (int it = 0; it < MG_EXP_COOP_ITERS; it++) {
-#ifndef MG_EXP_COOP_NOARB
+        for (int it = 0; it < MG_ITERATIONS; it++) {
             for (int i = 0; i < unact; i++) xarb_row<false>(R, V, rb0, lane, S, e, __builtin_amdgcn_readlane(apk, i), 0.0);
-#endif
-#ifdef MG_EXP_COOP_ARB2      // timing experiments only: the arbiter rows twice per iteration
-            for (int i = 0; i < unact; i++) xarb_row<false>(R, V, rb0, lane, S, e, __builtin_amdgcn_readlane(apk, i), 0.0);
-#endif
-#ifndef MG_EXP_COOP_NOGROUND
             if (G.n > 0) {
                 lground_apply(R, S, e, G.c0, dt);
                 if (G.n > 1) lground_apply(R, S, e, G.c1, dt);
             }
-#endif
-#ifndef MG_EXP_COOP_NOCONS
             rrows_apply(V, S, e, rc0, dt);
-#endif
-#ifdef MG_EXP_COOP_RR2       // timing experiments only: the robot rows twice per iteration
-            rrows_apply(V, S, e, rc0, dt);
-#endif
         }
         // robot lanes: velocities from V (their bias velocities stayed in the lanes)
         if (lane < nb) {
@@ -1864,7 +1807,6 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
         __syncthreads();
         return;
     }
-#endif
     for (int i = 0; i < unact; i++) larb_cached(R, lane, S, e, ufirst(AT(S.active, i)), dt_coef);
     if (G.n > 0) {
         lground_cached(R, S, e, G.c0, dt_coef);
@@ -1877,21 +1819,17 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
     }
     MG_PP(P, 5);
 #pragma unroll 1
-    for (int it = 0; it < MG_EXP_COOP_ITERS; it++) {
-#ifndef MG_EXP_COOP_NOARB
+    for (int it = 0; it < MG_ITERATIONS; it++) {
         for (int i = 0; i < unact; i++) larb_apply(R, lane, S, e, ufirst(AT(S.active, i)));
-#endif
         if (G.n > 0) {
             lground_apply(R, S, e, G.c0, dt);
             if (G.n > 1) lground_apply(R, S, e, G.c1, dt);
         }
-#ifndef MG_EXP_COOP_NOCONS
         for (int c = 0; c < unc; c++) {
             const int cb = ufirst(AT(S.cb, c));
             if (is_ground_row(G, cb)) continue;
             lcons_apply(R, lane, S, e, c, ufirst(AT(S.ca, c)), cb, ufirst(AT(S.ctype, c)), dt);
         }
-#endif
     }
     if (lane < nb) {
         AT(S.bvx, lane) = R.vx; AT(S.bvy, lane) = R.vy; AT(S.bw, lane) = R.w;

@@ -63,13 +63,6 @@ MG_DEV uint64_t qshfl_xor_u64(uint64_t u, int m) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-#ifdef MG_EXP_SAT2
-MG_DEV bool surely_apart_twice(const MGState &S, const mg_library *L, int e, int i, int j) {
-    int i2 = i;
-    asm volatile("" : "+v"(i2));   // an opaque copy: the compiler cannot merge the two tests
-    return surely_apart(S, L, e, i2, j) && true;
-}
-#endif
 // candidate k of shape i in the canonical order (walls 0..3, then shapes j = i + 1 + (k - 4)): the broadphase
 // tests that decide whether collide() runs -- cached BBs, shape filters (categories 0: MG_GROUP_OFF), same
 // body / same group, and the exact separating-axis skip
@@ -85,9 +78,6 @@ MG_DEV bool quad_candidate(const MGState &S, const mg_library *L, int e, int i, 
     const int j = i + 1 + (k - 4), gj = AT(S.sgroup, j);
     return al <= AT(S.sbbr, j) && AT(S.sbbl, j) <= ar && ab <= AT(S.sbbt, j) && AT(S.sbbb, j) <= at &&
            AT(S.sbody, j) != AT(S.sbody, i) && !((gi != 0 && gi == gj) || ((gi | gj) & MG_GROUP_OFF)) &&
-#ifdef MG_EXP_SAT2          // timing experiments only: the separating-axis test twice (idempotent)
-           !surely_apart_twice(S, L, e, i, j) &&
-#endif
            !surely_apart(S, L, e, i, j);
 }
 
@@ -108,9 +98,6 @@ MG_DEV void narrowphase_quad(const MGState &S, const mg_library *L, int e, int s
     for (int w0 = 0; w0 < ntot; w0 += 64) {
         const int wn = ntot - w0 < 64 ? ntot - w0 : 64;
         uint64_t hits = 0;
-#ifdef MG_EXP_PASS1X2       // timing experiments only: pass 1 twice (idempotent)
-        for (int rep = 0; rep < 2; rep++) { hits = 0;
-#endif
         {   // pass 1 (decode c -> (i, k) incrementally: candidates of one lane are QL apart)
             int i = 0, k = w0 + sub;
             while (i < ns && k >= 4 + ns - 1 - i) { k -= 4 + ns - 1 - i; i++; }
@@ -123,9 +110,6 @@ MG_DEV void narrowphase_quad(const MGState &S, const mg_library *L, int e, int s
 #pragma unroll
         for (int off = 1; off < QL; off <<= 1)   // the env's lanes: disjoint bits
             hits |= qshfl_xor_u64(hits, off);
-#ifdef MG_EXP_PASS1X2
-        }
-#endif
         // pass 2
         while (hits) {   // uniform over the env's lanes
             uint64_t rest = hits;
@@ -191,7 +175,6 @@ MG_DEV void space_step_quad(const MGState &S, const mg_library *L, int e, int su
     const uint32_t stamp = S.stamp[e] + 1;
     const int nact0 = S.nactive[e], nb = S.nbodies[e], ns = S.nshapes[e];
     for (int i = sub; i < nact0; i += QL) AT(S.astate, AT(S.active, i)) = ARB_NORMAL;
-#ifndef MG_EXP_NO_INTEGRATE  // timing experiments only (tools/build_unit_variant.sh): bodies never move
     for (int p = sub; p < nb; p += QL) {
         const int b = quad_body(p, nb);
         AT(S.bpx, b) = AT(S.bpx, b) + (AT(S.bvx, b) + AT(S.bvbx, b)) * dt;
@@ -199,15 +182,12 @@ MG_DEV void space_step_quad(const MGState &S, const mg_library *L, int e, int su
         body_set_angle_step(S, e, b, AT(S.ba, b) + (AT(S.bw, b) + AT(S.bwb, b)) * dt);
         AT(S.bvbx, b) = 0.0; AT(S.bvby, b) = 0.0; AT(S.bwb, b) = 0.0;
     }
-#endif
     __syncthreads();   // every lane has read the scalars; bodies before the shape BBs
     if (sub == 0) { S.stamp[e] = stamp; S.curr_dt[e] = dt; S.nactive[e] = 0; }
     for (int k = sub; k < ns; k += QL) shape_update_bb(S, L, e, k);
     __syncthreads();
     MG_PP(P, 1);
-#ifndef MG_EXP_NO_NARROW    // timing experiments only (tools/build_unit_variant.sh): no collisions at all
     narrowphase_quad<NCS, QL, LDS_SHAPES>(S, L, e, sub, ns);
-#endif
     __syncthreads();
     MG_PP(P, 2);
     for (int i = sub; i < S.arb_cap; i += QL) {   // cached arbiter filter
@@ -219,14 +199,8 @@ MG_DEV void space_step_quad(const MGState &S, const mg_library *L, int e, int su
     __syncthreads();
     MG_PP(P, 3);
     const int nact = S.nactive[e];
-#ifndef MG_EXP_NO_PRESTEP    // timing experiments only: no pre-steps
     for (int i = sub; i < nact; i += QL) arbiter_prestep(S, L, e, AT(S.active, i), dt);
     static_prestep_quad<NCS, QL>(S, e, sub, dt);
-#endif
-#ifdef MG_EXP_PRESTEP2      // timing experiments only: the constraint pre-steps twice
-    __syncthreads();
-    static_prestep_quad<NCS, QL>(S, e, sub, dt);
-#endif
     __syncthreads();
     MG_PP(P, 4);
     // velocity integration is the identity here (no gravity, damping 1, no forces)
@@ -255,12 +229,7 @@ __device__ __forceinline__ void env_substeps_quad(const MGState &V, const mg_lib
     for (int i = 0; i < 10; i++) {
         MG_PP(P, 0);
         space_step_quad<NCS, QL, LDS_SHAPES>(V, L, ev, sub, dt, P);   // starts with a workgroup barrier
-#ifndef MG_EXP_NO_RU         // timing experiments only: no robot update after the first
         if (sub == 0 && i < 9) robot_update<true>(V, L, ev);
-#endif
-#ifdef MG_EXP_RU2           // timing experiments only: the robot update twice (idempotent)
-        if (sub == 0 && i < 9) robot_update<true>(V, L, ev);
-#endif
     }
     __syncthreads();
 }

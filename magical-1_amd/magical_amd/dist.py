@@ -271,8 +271,11 @@ class GatheredStep:
     """Handle of one step's exchange: wait() orders the caller's current stream after it (the all-gather
     and, in gather_mode 'frames', the receiver-side restack)."""
 
-    def __init__(self, layout, recv, stacks, work=None, event=None):
+    def __init__(self, layout, recv, stacks, work=None, event=None, owner=None, step=None, windowed=False):
         self.layout, self.recv, self.stacks, self.work, self.event = layout, recv, stacks, work, event
+        # window-ring stacks (WindowRestacker) are views of one ring that the next exchange rewrites: remember
+        # which shard step made them so that a late results() raises instead of returning the next frames
+        self.owner, self.step, self.windowed = owner, step, windowed
 
     def wait(self):
         if self.work is not None:
@@ -286,6 +289,11 @@ class GatheredStep:
         """(obs dict of [W, n, ...] observation views, reward, done, info={'eval_score'[, 'target']}), all [W, n...]:
         observation keys and order as VecMagicalEnv returns them (PickAndPlace: allo, ego, target_type,
         target_colour, target_position[, past_obs])."""
+        if self.windowed and self.owner is not None and self.owner.t > self.step + 1:
+            raise RuntimeError(f"GatheredStep.results(): the stacked views of shard step {self.step} are window-ring "
+                               f"views, valid only until the next step_async() / reset_async() (the shard is at "
+                               f"step {self.owner.t}); read results() before issuing the next step, or build the "
+                               "ShardedVecEnv with window=False for stacks that stay valid for nbuf - 1 steps")
         self.wait()
         v = self.layout.unpack(self.recv)
         world, n = v["reward"].shape
@@ -475,13 +483,15 @@ class ShardedVecEnv:
                         t1.record(self.restack_stream)
                         self._restack_ev.append((t0, t1))
                     done_ev = self.restacked[b] = self.restack_stream.record_event()
-            h = GatheredStep(self.layout, recv, stacks, event=done_ev)
+            h = GatheredStep(self.layout, recv, stacks, event=done_ev, owner=self, step=step,
+                             windowed=stacks is not None and not getattr(self.restacker, "materialized", True))
         else:
             work = dist.all_gather_into_tensor(recv, send, async_op=True)
             work.wait()
             if stacks is not None:
                 stacks = self.restacker(recv, stacks, step, all_fresh) or stacks
-            h = GatheredStep(self.layout, recv, stacks)
+            h = GatheredStep(self.layout, recv, stacks, owner=self, step=step,
+                             windowed=stacks is not None and not getattr(self.restacker, "materialized", True))
         self.pending[b] = h
         self.t += 1
         return h

@@ -283,6 +283,13 @@ class VecMagicalEnv:
                                             ctypes.c_void_p(counts.data_ptr()), self._stream()))
         return out, counts
 
+    def step_form(self):
+        """(form, envs per workgroup, (bodies, shapes, constraints, arbiter slots) caps) of the step kernel
+        (mg_step_form)"""
+        out = (ctypes.c_int32 * 6)()
+        native.check(self.lib.mg_step_form(self.handle, out))
+        return int(out[0]), int(out[1]), tuple(int(x) for x in out[2:6])
+
     def arbiters(self):
         """solved arbiters per env in active order: f64 [N, 48, 28] and contact hashes u64 [N, 48, 2]
         (mg_get_arbiters; the active count is bodies()[1][:, 3])"""

@@ -13,7 +13,7 @@ if os.environ.get("MAGICAL_AMD_EXP_LIB"):   # A/B kernel experiments (tools/gpu_
     LIB_PATH = os.path.join(HERE, "libmagical_sim_%s.so" % os.path.basename(os.environ["MAGICAL_AMD_EXP_LIB"]))
 
 EXPORTS = ["mg_create", "mg_bind_outputs", "mg_reset", "mg_step", "mg_render_full", "mg_get_bodies", "mg_get_arbiters",
-           "mg_set_body_pose", "mg_get_errors", "mg_seed", "mg_random_actions", "mg_num_envs", "mg_enable_timing", "mg_read_timing",
+           "mg_set_body_pose", "mg_get_errors", "mg_seed", "mg_random_actions", "mg_num_envs", "mg_step_form", "mg_enable_timing", "mg_read_timing",
            "mg_set_episode_steps", "mg_selftest_sincos", "mg_replay_lores", "mg_restack", "mg_restack_window", "mg_bind_window",
            "mg_window_start", "mg_destroy", "mg_last_error"]
 
@@ -47,6 +47,14 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise NativeError(f"{LIB_PATH} not found: build it with `python -m magical_amd.build` "
                           "(no CPU fallback exists for the simulator)")
+    if os.path.basename(LIB_PATH) != "libmagical_sim.so":
+        # a profiling / experiment variant (MAGICAL_AMD_PROFILE, MAGICAL_AMD_EXP_LIB) is built by hand: refuse one
+        # older than the sources, so no profile is taken on a stale build
+        csrc = os.path.join(os.path.dirname(HERE), "csrc")
+        newest = max(os.path.getmtime(os.path.join(csrc, f)) for f in os.listdir(csrc))
+        if os.path.getmtime(LIB_PATH) < newest:
+            raise NativeError(f"{LIB_PATH} is older than magical-1_amd/csrc: rebuild it (python -m magical_amd.build "
+                              "--profile, or tools/build_unit_variant.sh) before profiling with it")
     lib = ctypes.CDLL(LIB_PATH)
     vp, i32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64
     lib.mg_create.argtypes = [ctypes.POINTER(mg_config), ctypes.POINTER(vp)]
@@ -62,6 +70,8 @@ def load():
     lib.mg_seed.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
     lib.mg_random_actions.argtypes = [vp, vp, u64, u64, vp]
     lib.mg_num_envs.argtypes = [vp]
+    if hasattr(lib, "mg_step_form"):
+        lib.mg_step_form.argtypes = [vp, vp]
     lib.mg_selftest_sincos.argtypes = [vp, vp, vp, i32, vp]
     lib.mg_enable_timing.argtypes = [vp, i32]
     lib.mg_read_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]

@@ -501,6 +501,20 @@ def test_bench_byte_models():
     assert s["bytes_per_env_step"] == 223232 and s["traffic_ratio_basis_bytes_per_env_step"] == 2048
     assert 255 < s["traffic_ratio"] < 265
     assert bench.kernel_record("step_kernel", 1.0, "LoRes4E", 64, None)["traffic_ratio"] is None
+    # the step kernel's design bytes: its HBM <-> LDS state transfer at the form's slot caps (csrc/mg_stepk.h),
+    # 209 B per live arbiter slot each way; the traffic ratio is then over those
+    assert bench.step_state_bytes(5, (6, 5, 10, 20), 0) == 2509      # MoveToRegion, quad form
+    assert bench.step_state_bytes(6, (7, 6, 12, 32), 0) == 3011      # MoveToCorner
+    assert bench.step_state_bytes(4, (14, 53, 26, 48), 0) == 6939    # the many-block scenes, cooperative form
+    assert bench.step_state_bytes(4, (14, 53, 26, 48), 2.5) == 6939 + round(2.5 * 2 * 209)
+    s = bench.kernel_record("step_kernel", 2.7, "LoResStack", 8192, {"bytes_per_launch": 98e6}, step_bytes=6939)
+    assert s["kernel_bytes_per_env_step"] == 6939 and s["traffic_ratio_basis_bytes_per_env_step"] == 6939
+    assert abs(s["traffic_ratio"] - 98e6 / (6939 * 8192)) < 0.01
+    os.environ["MG_STEP_VARIANT"] = "4"
+    try:
+        assert bench.env_overrides().get("MG_STEP_VARIANT") == "4"
+    finally:
+        del os.environ["MG_STEP_VARIANT"]
 
 
 GATHER_CASES = [("MoveToRegion-Demo-LoRes4E-v0", "frames"), ("MoveToRegion-Demo-LoRes4E-v0", "stacked"),
@@ -639,3 +653,18 @@ def test_pipeline_default_chunks():
     assert pipeline.default_chunks(registry.lookup("MoveToRegion-Demo-LoRes4E-v0"), 64) == 1
     assert pipeline.default_chunks(registry.lookup("ClusterColour-Demo-LoResStack-v0"), 8192) == 1
     assert pipeline.default_chunks(registry.lookup("MatchRegions-TestAll-LoRes4E-v0"), 8192) == 1
+
+
+def test_gathered_window_views_raise_when_stale():
+    """a step's window-ring stacks are rewritten by the next exchange, so results() of an older
+    GatheredStep raises once its shard has issued a later step_async / reset_async (materialised stacks and
+    frames-only results are not affected)."""
+    class Owner:
+        t = 1
+    h = mdist.GatheredStep(None, None, {"past_obs": None}, owner=Owner, step=0, windowed=True)
+    Owner.t = 2
+    with pytest.raises(RuntimeError, match="window-ring"):
+        h.results()
+    h2 = mdist.GatheredStep(None, None, {}, owner=Owner, step=0, windowed=False)
+    with pytest.raises(AttributeError):   # no guard: it goes on to unpack (None layout here)
+        h2.results()
