@@ -425,19 +425,21 @@ def main():
     form, blk, caps = sim0.step_form()
     live = float(sim0.bodies()[1][:, 3].double().mean().item())   # active arbiters per env after the timed run
     step_bytes = step_state_bytes(form, caps, live)
-    # The timed launches' HIP-event times are co-running figures: chunked runs overlap the other chunk's kernels,
-    # and the many-block scenes' next-layout shadow (reset_kernel on the simulator's side stream) co-runs with
-    # the step and render kernels.  The roofline's per-kernel times come from an isolated pass after the timed
-    # region: one simulator (chunk 0 of a pool) stepped alone, the device synchronised before every step, so its
-    # step kernel has nothing beside it (the shadow's launch follows the step kernel and overlaps the render,
-    # as in every step), args.iso_steps steps of the same env count per launch.
+    # chunked runs: the timed launches overlap the other chunk's kernels, so their HIP-event times are
+    # co-running figures.  The roofline's per-kernel times come from an isolated pass after the timed region:
+    # chunk 0 stepped alone (its step, reset and render kernels back to back on one stream, nothing beside
+    # them), args.iso_steps steps of the same env count per launch.  Unchunked runs keep the timed launches (one
+    # stream; the many-block scenes' next-layout shadow co-runs on the simulator's side stream in every step, as
+    # in steady-state use).  Round 6: an isolated pass for them too (the device synchronised before each step)
+    # measured the cooperative step kernel 5% LONGER than the timed launches (2.84 vs 2.70 ms, ClusterColour), and
+    # under rocprofv3 the same HIP events read 2.47 / 2.58 ms against rocprof's 2.45 / 2.54 ms -- the events
+    # agree with the profiler within the same run, and the profiler itself shortens that kernel by ~10%.
     iso = None
-    if args.iso_steps > 0:
+    if chunks > 1 and args.iso_steps > 0:
         native.check(lib.mg_enable_timing(sim0.handle, args.iso_steps))
         a0 = torch.empty(sim0.num_envs, dtype=torch.uint8, device=device)
         for s in range(args.iso_steps):
             sim0.random_actions(10 ** 6 + s, out=a0)
-            torch.cuda.synchronize(device)
             sim0.step(a0)
         torch.cuda.synchronize(device)
         ti = (ctypes.c_double * 4)()
@@ -473,8 +475,7 @@ def main():
             "step_kernel": kernel_record("step_kernel", k_step, spec.preproc, units, pmc_for("step_kernel"),
                                          step_bytes=step_bytes),
             "reset_kernel": {"ms": round(k_reset, 4)},
-            "timing": ("isolated (after the timed region: " + ("chunk 0" if chunks > 1 else "the simulator") +
-                       " stepped alone, device synchronised before each step)") if iso else "timed launches (one stream)",
+            "timing": "isolated (chunk 0 alone after the timed region)" if iso else "timed launches (one stream)",
             "step_form": {"form": form, "envs_per_workgroup": blk, "caps_bodies_shapes_constraints_arbiters": caps,
                           "live_arbiters_per_env": round(live, 3), "state_bytes_per_env_step": step_bytes},
         }

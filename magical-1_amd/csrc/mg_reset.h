@@ -22,7 +22,49 @@ MG_DEV void mt_seed(const MGState &S, int e, uint32_t seed) {
     }
     S.mt_pos[e] = 624;
 }
+// The twist over the LDS copy (a cooperative reset: the wave's 64 lanes call mt_next32 together with the same
+// state).  Word i's new value reads the old words i, i + 1 and, for i < 227, the old word i + 397, else the NEW
+// word i - 227; so the words are updated in order in chunks of 64 lanes -- each chunk's loads precede its stores
+// (one wave, in-order LDS), its i + 1 / i + 397 words are not yet rewritten and its i - 227 words were rewritten
+// by an earlier chunk -- and word 623 last (new words 396 and 0).  Same values as the serial loop below.
+MG_DEV void mt_twist_lds(uint32_t *m) {
+    const uint32_t UPPER = 0x80000000u, LOWER = 0x7fffffffu, MA = 0x9908b0dfu;
+    if (__builtin_amdgcn_read_exec() == ~0ull) {
+        const int lane = (int)(threadIdx.x & 63);
+        for (int b = 0; b < 623; b += 64) {
+            const int i = b + lane;
+            uint32_t v = 0u;
+            if (i < 623) {
+                const uint32_t y = (m[i] & UPPER) | (m[i + 1] & LOWER);
+                v = m[i < 227 ? i + 397 : i - 227] ^ (y >> 1) ^ (-(y & 1u) & MA);
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (i < 623) m[i] = v;
+            __builtin_amdgcn_wave_barrier();
+        }
+    } else {   // (not every lane active: each runs the serial twist, writing the same values)
+        for (int i = 0; i < 623; i++) {
+            const uint32_t y = (m[i] & UPPER) | (m[i + 1] & LOWER);
+            m[i] = m[i < 227 ? i + 397 : i - 227] ^ (y >> 1) ^ (-(y & 1u) & MA);
+        }
+    }
+    const uint32_t y = (m[623] & UPPER) | (m[0] & LOWER);
+    m[623] = m[396] ^ (y >> 1) ^ (-(y & 1u) & MA);
+}
 MG_DEV uint32_t mt_next32(const MGState &S, int e) {
+    if (S.mt_lds) {   // the cooperative reset's LDS copy (every lane reads and writes the same words)
+        uint32_t *m = S.mt_lds;
+        int pos = (int)m[624];
+        if (pos == 624) { mt_twist_lds(m); pos = 0; }
+        uint32_t y = m[pos];
+        __builtin_amdgcn_wave_barrier();
+        m[624] = (uint32_t)(pos + 1);
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= (y >> 18);
+        return y;
+    }
     int pos = S.mt_pos[e];
     if (pos == 624) {
         const uint32_t UPPER = 0x80000000u, LOWER = 0x7fffffffu, MA = 0x9908b0dfu;

@@ -62,6 +62,9 @@ struct MGState {
     // ---- RNG: numpy legacy MT19937 per env ----
     uint32_t *mt_key;        // [624][N]
     int32_t *mt_pos;         // [N]
+    // the env's MT19937 state cached in the wave's LDS during a cooperative reset (reset_kernel): key[0..623],
+    // [624] = pos; null: draws go to mt_key / mt_pos in HBM (the step kernel's fused resets)
+    uint32_t *mt_lds;
     // ---- LoRes frame history (downsampled, newest last) ----
     uint8_t *hist_allo;      // [4][N][96*96*3]
     uint8_t *hist_ego;       // [4][N][96*96*3]
