@@ -1557,10 +1557,15 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
         i = lo;
         r = p - pair_row_off(i, ns);
     };
+    // a round that fills up stops its pass 1 at the chunk holding its last hit; the next round resumes there
+    // (it used to rescan every chunk from pair 0)
+    int base0 = 0, seen0 = 0;
     for (int round0 = 0;; round0 += 64) {   // hits [round0, round0 + 64) of the substep's canonical hit list
         int mine = 0;                        // 1 + the pair index of this lane's hit in the round (0: none)
-        int seen = 0;                        // hits of the chunks tested so far (wave-uniform)
-        for (int base = 0; base < total; base += 64) {
+        int seen = seen0;                    // hits of the chunks before `base` (wave-uniform)
+        bool more = false;                   // this round is full: another one follows
+        int base = base0;
+        for (; base < total; base += 64) {
             const int p = base + lane;
             bool hit = false;
             if (p < total) {
@@ -1593,8 +1598,10 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
                 }
                 mine = base + lo + 1;
             }
+            if (seen + nm >= round0 + 64) { more = true; break; }   // the next round's hits start in this chunk
             seen += nm;
         }
+        base0 = base; seen0 = seen;
         int i = 0, j = 0;
         Collision info;
         info.count = 0;
@@ -1642,7 +1649,7 @@ MG_DEV void space_step_coop(const MGState &S, const mg_library *L, double dt, in
             }
         }
         MG_PP(P, 9);
-        if (seen <= round0 + 64) break;   // every hit of the substep has been collided
+        if (!more) break;   // every hit of the substep has been collided
     }
 #else
     // pair p (canonical order) on lane p mod 64

@@ -13,8 +13,16 @@
 // slot caps of every compiled form: the LDS variants of mg_launch.h, plus the QL-lanes-per-env forms of the
 // compile-time scenes (5: the caps of 1 with two world-shape slots per lane in LDS -- 2 x 64 per workgroup,
 // so 128 / blk per env; 6: the caps of 2, world shapes in per-lane locals as there)
+// Form 5's narrowphase operands (two ShapeW per lane) in LDS (1, rounds 2-5) or per-lane locals (0, round 6, as
+// form 6).  The LDS slots were 51 of the 8-env workgroup's 78 KB; without them the step workgroup takes 27 KB, so
+// more of the other chunk's render workgroups co-run beside it: step kernel 0.400 -> 0.415 ms alone, 0.61 -> 0.52 ms
+// co-running, MoveToRegion 3.04 -> 3.16 M env-steps/s (profiles/r06_q5)
+#ifndef MG_Q5_LDS_SHAPES
+#define MG_Q5_LDS_SHAPES 0
+#endif
 __host__ __device__ constexpr StepCaps step_form_caps(int v, int blk) {
-    return v == 5 ? StepCaps{6, 5, 10, 20, 16, 128 / blk} : v == 6 ? StepCaps{7, 6, 12, 32, 16, 0} : step_variant_caps(v);
+    return v == 5 ? StepCaps{6, 5, 10, 20, 16, MG_Q5_LDS_SHAPES ? 128 / blk : 0}
+         : v == 6 ? StepCaps{7, 6, 12, 32, 16, 0} : step_variant_caps(v);
 }
 
 // ---- LDS-resident substeps ------------------------------------------------

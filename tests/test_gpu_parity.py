@@ -440,18 +440,22 @@ def test_window_stacks_match_materialised(name, n, L):
                                           ("MoveToCorner-Demo-LoRes4E-v0", 4096, 165)])
 def test_full_size_pipelined_parity(name, n, steps):
     """The configuration bench.py times for C2 / C3: magical_amd.pipeline.PipelinedVecEnv
-    with 2 chunks of 2048 envs (the 8-envs-per-workgroup step forms 5 / 6 and the auto-reset fused into the
-    step kernel), episode phases spread over the envs the oracle does not follow (so every step mixes resetting
-    and running envs in a workgroup), against the oracle every step on a spread of envs of both chunks:
-    observations bit-exact, body state within POSE_TOL, done / eval_score equal, >= 2 episode boundaries."""
+    with bench.py's own chunking (pipeline.default_chunks: 3 chunks of ~1365 envs for MoveToRegion, 2 of 2048
+    for MoveToCorner; the 8-envs-per-workgroup step forms 5 / 6 and the auto-reset fused into the step kernel),
+    episode phases spread over the envs the oracle does not follow (so every step mixes resetting and running
+    envs in a workgroup), against the oracle every step on a spread of envs of every chunk: observations
+    bit-exact, body state within POSE_TOL, done / eval_score equal, >= 2 episode boundaries."""
     from magical_amd import pipeline
     spec = registry.lookup(name)
     L = spec.max_episode_steps
     seeds = [1000 + i for i in range(n)]
-    pool = pipeline.PipelinedVecEnv(name, n, chunks=2, seeds=seeds)
-    assert [s.num_envs for s in pool.sims] == [n // 2, n // 2]
-    h = n // 2
-    pick = sorted({0, 1, 7, 8, 63, 64, h - 1, h, h + 1, h + 9, n - 9, n - 1})
+    chunks = pipeline.default_chunks(spec, n)
+    pool = pipeline.PipelinedVecEnv(name, n, chunks=chunks, seeds=seeds)
+    assert chunks >= 2 and sum(s.num_envs for s in pool.sims) == n
+    pick = {0, 1, 7, 8, 63, 64, n - 9, n - 1}
+    for b in pool.bounds[1:-1]:   # both sides of every chunk boundary
+        pick |= {b - 1, b, b + 1, b + 9}
+    pick = sorted(pick)
     orc = {i: po.OracleEnv(spec.task, spec.rand_flags, spec.preproc, L, seed=seeds[i]) for i in pick}
     obs = pool.reset()
     pool.wait()

@@ -627,3 +627,4 @@ def test_gpu_narrowphase_twin(name, n, env, monkeypatch):
     print(name, env, seen, "EPA runs", epa_runs() - e0)
     assert int(vec.errors().abs().sum().item()) == 0
     vec.close()
+
