@@ -199,11 +199,12 @@ def cpu_baseline(name, workers, steps, affinity, quota):
 
 def load_pmc(kernel, workload, envs, envs_per_launch=None):
     """PMC record of `kernel` (HBM bytes per launch, VALU issue fraction) from the committed passes, newest
-    first: profiles/r05_final/<workload>.traffic.json (tools/gpu_table.sh at the round's final build), then
+    first: profiles/r06_final/<workload>.traffic.json (tools/gpu_table.sh at the round's final build), then
     the earlier rounds' -- only when collected on this workload, env count and envs per launch (records without
     envs_per_launch were collected unchunked: envs per launch = envs)."""
     epl = envs if envs_per_launch is None else envs_per_launch
-    for path in (os.path.join(ROOT, "profiles", "r05_final", f"{workload}.traffic.json"),
+    for path in (os.path.join(ROOT, "profiles", "r06_final", f"{workload}.traffic.json"),
+                 os.path.join(ROOT, "profiles", "r05_final", f"{workload}.traffic.json"),
                  os.path.join(ROOT, "profiles", "r04_final", f"{workload}.traffic.json"),
                  os.path.join(ROOT, "profiles", "r03_final", f"{workload}.traffic.json"),
                  os.path.join(ROOT, "profiles", "r02_final", f"{workload}.traffic.json"),

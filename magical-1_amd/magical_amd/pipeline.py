@@ -33,13 +33,11 @@ PIPELINED_TASKS = ("MoveToRegion", "MoveToCorner")
 
 
 def default_chunks(spec, num_envs):
-    """bench.py --chunks auto: 2 for the robot scenes at >= 2048 envs (MoveToRegion: 3 at >= 3072 envs), else 1.
-    Round 6: with form 5's narrowphase operands out of LDS its step workgroups take 54 instead of 102 KB, the
-    step kernels hide behind the other chunks' renders, and a third MoveToRegion chunk measured 3.16 -> 3.19 M
-    env-steps/s at 4096 envs (MoveToCorner, step-bound: 2 chunks as before; profiles/r06_d)."""
-    if spec.task not in PIPELINED_TASKS or num_envs < 2048 or num_envs % 2:
-        return 1
-    return 3 if spec.task == "MoveToRegion" and num_envs >= 3072 else 2
+    """bench.py --chunks auto: 2 for the robot scenes at >= 2048 envs, else 1.  (Round 6: a third MoveToRegion
+    chunk measured 3.16 -> 3.19 M env-steps/s at 4096 envs, within 1%, but its 1365-env renders fill 1.2 rounds of
+    the CUs' workgroup slots, so the dominant kernel's isolated HBM fraction reads 0.061 instead of 0.069; kept
+    at 2, profiles/r06_d, profiles/r06_final.)"""
+    return 2 if spec.task in PIPELINED_TASKS and num_envs >= 2048 and num_envs % 2 == 0 else 1
 
 
 class PipelinedVecEnv:
