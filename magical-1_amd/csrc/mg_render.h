@@ -13,7 +13,7 @@
 // rule "last primitive drawn wins" is "largest ordinal wins" -- and one thread
 // per 4x4 block resolves fills (geoms in draw order), takes the max with the
 // outline layer, looks up colours and sums the block (cv2 INTER_AREA 4x:
-// round-half-even of sum/16).  Each band yields 2 LoRes rows written to HBM
+// round-half-even of sum/16).  Each band yields RG_BAND / 4 LoRes rows written to HBM
 // with 16-byte stores, together with the frame-stack ring.
 #pragma once
 #include "mg_launch.h"
@@ -23,8 +23,13 @@
 
 // capacity classes (template parameters of the LDS layout): geoms, vertices, dash lines, bin entries
 // (outline items + fill edges, binned per band), solid outline edges, entities, outline-mask type (one bit
-// per entity).  The large class fits every task; the small one fits robot + arena + goal + one block
-// (MoveToRegion / MoveToCorner) and leaves room for 9 workgroups/CU.
+// per entity), rows per band (default 8), outline-mask bits per pixel (default: the type's).  The large class
+// fits every task; the small one fits robot + arena + goal or one block (MoveToRegion / MoveToCorner: at most
+// 26 geoms (star block), 636 vertices (circle block), 204 solid outline edges, 3 entities) in 16-row bands with
+// a 4-bit outline mask: 17.4 KB, 9 workgroups/CU (round 6: the 8-row class took 16.2 KB at 9 per CU; 16-row bands
+// halve the bands' barriers, band lists and per-band edge / segment set-up, render 0.628 -> 0.553 ms per 2048-env
+// chunk, MoveToRegion 3.16 -> 3.37 M env-steps/s, profiles/r06_b16).  The many-block classes stay at 8 rows:
+// 16-row medium-0 / medium-1 (6 / 5 per CU) measured 15% / 6% slower (ClusterColour / MatchRegions).
 #define RG_LARGE 160, 1600, 256, 3072, 1600, MG_MAX_ENTS, uint32_t
 #ifndef RG_MEDIUM0
 #define RG_MEDIUM0 44, 784, 128, 1280, 512, MG_MAX_ENTS, uint16_t   // 20.3 KB: 8 workgroups/CU
@@ -33,12 +38,12 @@
 #define RG_MEDIUM1 48, 896, 160, 1536, 512, MG_MAX_ENTS, uint16_t
 #endif
 #define RG_MEDIUM2 96, 1280, 160, 2560, 768, MG_MAX_ENTS, uint16_t
-#define RG_SMALL 32, 704, 160, 1536, 256, 6, uint8_t
+#ifndef RG_SMALL
+#define RG_SMALL 28, 640, 160, 1536, 208, 4, uint8_t, 16, 4
+#endif
 #define RG_MAXLONG 16
 #define RG_MAXDE 16                     // dashed edges whose dashes are split over the workgroup
-#define RG_BAND 8
-#define RG_NBANDS (MG_RES / RG_BAND)
-#define RG_THREADS 192                  // = one thread per 4x4 block of a band (2 x 96)
+#define RG_THREADS 192                  // = one thread per 4x4 block of a band's first 2 block rows (2 x 96)
 #ifndef RG_SHORT
 #define RG_SHORT 12                     // segments with <= RG_SHORT * RG_SEGLANES pixels in a band: drawn by
 #endif
@@ -65,8 +70,6 @@
 #define RG_EMPTY 32767
 #define RG_OSH (RG_OFS ? 3 : 0)         // resolve/outline-layer ordinal values are ordinal << RG_OSH
 #define RG_LOROW (MG_LORES * 3)         // bytes of one 96-px RGB row
-#define RG_BANDLO (2 * RG_LOROW)        // bytes of the 2 LoRes rows one band produces
-#define RG_BANDLO16 (RG_BANDLO / 16)    // ... in 16-byte chunks (36)
 
 // q = n / d and r = n % d for 0 <= n < 2^31, 1 <= d: a float reciprocal estimate (relative error below
 // 2^-22, so q is off by at most one for n < 2^22) corrected by one step; larger n take the integer divide
@@ -88,18 +91,22 @@ MG_DEV int udivmod(int n, int d, int &r) {
 struct LineK { int x1, y1, sgx, sgy, DX, DY, xmaj; };
 
 // LDS: the setup matrices / scratch and the band buffers are never live at the same time, so they
-// share storage.  Small class: 9 workgroups per CU (< 17 KiB); large class: 3.
+// share storage.  Small class: 9 workgroups per CU (17.4 KB); large class: 3.
 //
 // Outline layer, MT = u32: the largest outline ordinal drawn at each pixel (atomicMax).  MT = u8: every
 // entity draws at most one outlined polygon (the library builder checks it), and entities are drawn in
 // add order, so "largest outline ordinal at a pixel" is "highest entity bit set at the pixel": the
-// layer holds one bit per entity (atomicOr on words of 4 pixels) and oord[] maps the entity back to its
-// outline's ordinal -- a quarter of the LDS.
-template <int MAXG_, int MAXVERT_, int MAXDASH_, int MAXBIN_, int MAXSEDGE_, int MAXE_, typename MT_>
+// layer holds one bit per entity (atomicOr on words of 4 pixels; 8 pixels of 4 bits for the small class's
+// <= 4 entities) and oord[] maps the entity back to its outline's ordinal -- a quarter (an eighth) of the LDS.
+template <int MAXG_, int MAXVERT_, int MAXDASH_, int MAXBIN_, int MAXSEDGE_, int MAXE_, typename MT_, int BAND_ = 8,
+          int MBITS_ = 8 * (int)sizeof(MT_)>
 struct RenderSmem {
     static constexpr int RG_MAXG = MAXG_, RG_MAXVERT = MAXVERT_, RG_MAXDASH = MAXDASH_, RG_MAXBIN = MAXBIN_,
                          RG_MAXSEDGE = MAXSEDGE_, RG_MAXE = MAXE_;
-    static constexpr int MBITS = 8 * (int)sizeof(MT_), MPW = 4 / (int)sizeof(MT_);   // bits / pixels per word
+    static constexpr int MBITS = MBITS_, MPW = 32 / MBITS_;   // bits / pixels per word of the outline layer
+    static_assert(BAND_ == 8 || BAND_ == 16, "bands of 8 or 16 rows");
+    static constexpr int BAND = BAND_, NBANDS = MG_RES / BAND_, BROWS = BAND_ / 4;   // rows, bands, LoRes rows per band
+    static constexpr int BANDLO16 = BROWS * RG_LOROW / 16;   // 16-byte chunks of a band's LoRes rows (36 / 72)
     static constexpr uint32_t MMASK = (1u << MBITS) - 1u;
     static constexpr bool ORDMAX = MBITS == 32;                                      // layer of ordinals
     static_assert(ORDMAX || (MAXE_ <= MBITS && MAXE_ <= MG_MAX_ENTS), "one outline-mask bit per entity");
@@ -111,7 +118,7 @@ struct RenderSmem {
             // setup scratch (dead before the bands)
             int32_t gbb[RG_MAXG][4];                 // per-geom ymin, ymax, xmin, xmax while built (atomics)
             int32_t gchg[RG_MAXG];                   // direction changes of the y sequence around each polygon
-            int32_t bin_cnt[RG_NBANDS], ebin_cnt[RG_NBANDS];
+            int32_t bin_cnt[NBANDS], ebin_cnt[NBANDS];
             int16_t g_rpoly[RG_MAXG];
             int16_t e_g0[RG_MAXE + 1];
             int16_t e_r0[RG_MAXE];                   // first render poly of each entity
@@ -121,20 +128,20 @@ struct RenderSmem {
             int32_t ndedge;
         } pre;
         struct {
-            uint32_t band[RG_BAND][MG_RES / MPW]; // outline layer of the current band (entity bits per pixel)
-            uint4 lo[RG_BANDLO16];          // current frame, 2 LoRes rows
+            uint32_t band[BAND][MG_RES / MPW]; // outline layer of the current band (entity bits per pixel)
+            uint4 lo[BANDLO16];          // current frame, the band's LoRes rows
             union {
                 struct {
                     int32_t lk[RG_MAXLONG][7];      // long segments of this band (LineK)
                     int32_t lkr[RG_MAXLONG][3];     // klo, khi, ordinal
                 };
-                uint4 los[RG_BANDLO16];     // the band's static-layer rows (episode's first allo frame; written
+                uint4 los[BANDLO16];     // the band's static-layer rows (episode's first allo frame; written
                                             // after the long segments are drawn, read in the band's tail)
             };
         } post;
     } u;
     uint2 ginfo[RG_MAXG];                     // (ymin | ymax << 16, xmin | xmax << 16), int16 halves
-    uint32_t bspan[RG_MAXG][RG_BAND];         // spans of the band's rows, per band-list slot: l | r << 16
+    uint32_t bspan[RG_MAXG][BAND];         // spans of the band's rows, per band-list slot: l | r << 16
     uint64_t col[2 * RG_MAXG + 2];            // R | G << 16 | B << 32 per ordinal
     int16_t g_voff[RG_MAXG + 1], g_nv[RG_MAXG];
     int16_t vx[RG_MAXVERT], vy[RG_MAXVERT];   // int pixel vertices (pygame (int) truncation)
@@ -147,8 +154,8 @@ struct RenderSmem {
     uint16_t dash_o[RG_MAXDASH];              // outline-layer value of each dash line
     int8_t g_ent[RG_MAXG];
     uint16_t oord1[17];                       // [k + 1]: ordinal of entity k's outlined polygon (0: none)
-    int16_t bin_off[RG_NBANDS + 1];           // per-band outline item lists (in bin[])
-    int16_t ebin_off[RG_NBANDS + 1];          // per-band fill edge lists (in bin[], after the outline items)
+    int16_t bin_off[NBANDS + 1];           // per-band outline item lists (in bin[])
+    int16_t ebin_off[NBANDS + 1];          // per-band fill edge lists (in bin[], after the outline items)
     uint16_t bin[RG_MAXBIN];                  // outline item index, or fill edge: vertex | closing << 14 | last-row << 15
     int16_t gslot[RG_MAXG];                   // band-list slot of each geom overlapping the current band
     int32_t ngeom, nsedge, ndash, nlong, nblist, err;
@@ -297,7 +304,7 @@ MG_DEV void push_dash(SM &sm, const DashSeq &d, int k, int ord) {
 template <class SM>
 MG_DEV void band_put(SM &sm, int x, int y, int y0, uint32_t obit) {
     int r = y - y0;
-    if (r >= 0 && r < RG_BAND && x >= 0 && x < MG_RES) {
+    if (r >= 0 && r < SM::BAND && x >= 0 && x < MG_RES) {
         if constexpr (SM::ORDMAX) atomicMax(&sm.u.post.band[r][x], obit);
         else atomicOr(&sm.u.post.band[r][x / SM::MPW], obit << (SM::MBITS * (x % SM::MPW)));
     }
@@ -312,11 +319,12 @@ MG_DEV LineK line_k(int x1, int y1, int x2, int y2) {
     return {x1, y1, sgx, sgy, DX, DY, DX >= DY ? 1 : 0};
 }
 
-// the k-range [klo, khi] of a segment's pixels inside rows [y0, y0 + RG_BAND)
+// the k-range [klo, khi] of a segment's pixels inside rows [y0, y0 + BAND)
+template <int BAND>
 MG_DEV void band_krange(const LineK &L, int y0, int &klo, int &khi) {
     // row index along the segment (m for x-major, k for y-major) in [0, DY)
-    int mlo = L.sgy > 0 ? y0 - L.y1 : L.y1 - (y0 + RG_BAND - 1);
-    int mhi = mlo + RG_BAND - 1;
+    int mlo = L.sgy > 0 ? y0 - L.y1 : L.y1 - (y0 + BAND - 1);
+    int mhi = mlo + BAND - 1;
     mlo = mlo > 0 ? mlo : 0;
     mhi = mhi < L.DY - 1 ? mhi : L.DY - 1;
     if (L.xmaj) {
@@ -350,7 +358,7 @@ template <class SM>
 MG_DEV void segment_band(SM &sm, int x1, int y1, int x2, int y2, uint32_t ord, int y0, int sub) {
     int klo, khi;
     const LineK L = line_k(x1, y1, x2, y2);
-    band_krange(L, y0, klo, khi);
+    band_krange<SM::BAND>(L, y0, klo, khi);
     if (khi < klo) return;
     const int n = khi - klo + 1;
     if (n <= RG_SHORT * RG_SEGLANES) {
@@ -481,6 +489,13 @@ __global__ void __launch_bounds__(RG_THREADS)
 __attribute__((amdgpu_waves_per_eu((SM::RG_MAXG <= 32 && RG_SMALL_WPE) ? RG_SMALL_WPE : 1)))
 render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     __shared__ SM sm;
+    // band geometry of the class: rows per band, LoRes rows per band (a thread resolves RG_BROWS / 2 blocks),
+    // frame-stack threads (4 pixels each), first ring / plain writer thread, the band's LoRes bytes and 16-byte
+    // chunks, first static-layer prefetch thread
+    constexpr int RG_BAND = SM::BAND, RG_NBANDS = SM::NBANDS, RG_BROWS = SM::BROWS;
+    constexpr int RG_STKT = RG_BROWS * MG_LORES / 4, RG_RING0 = RG_STKT > 64 ? RG_STKT : 64;
+    constexpr int RG_BANDLO = RG_BROWS * RG_LOROW, RG_BANDLO16 = SM::BANDLO16;
+    constexpr int RG_CPF0 = RG_THREADS - RG_BANDLO16 < 128 ? RG_THREADS - RG_BANDLO16 : 128;
     constexpr int mode = MODE == 2 ? 0 : MODE;
     constexpr bool WIN = MODE == 2;
     const int e = blockIdx.x, view = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
@@ -845,9 +860,10 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     uint8_t *o_stack = pp == MG_PREPROC_LORESSTACK ? o_plain : out.obs_past;
     // 4x4 block of this thread: wave w covers block columns [32w, 32w + 32) of both block rows, so a
     // geom's x-range meets few waves and the per-geom fill test is skipped wave-wide elsewhere
-    const int oyl = lane >> 5, ox = 32 * (tid >> 6) + (lane & 31), x0 = 4 * ox, lpix = oyl * MG_LORES + ox;
+    // (16-row bands: block rows oyl and oyl + 2)
+    const int oyl = lane >> 5, ox = 32 * (tid >> 6) + (lane & 31), x0 = 4 * ox;
     // frame-stack threads (4 pixels each) hold frames t-3..t-1 of their pixels in registers
-    const bool do_pf = mode == 0 && stacked && !fresh && tid < 2 * MG_LORES / 4;
+    const bool do_pf = mode == 0 && stacked && !fresh && tid < RG_STKT;
 #ifdef MG_PROFILE
     const int dskip = out.debug_skip;
 #else
@@ -923,8 +939,8 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         b1 = y0 <= y1 ? y1 / RG_BAND + 1 : 0;
     };
     auto cache_prefetch = [&](int y0) {
-        if (use_cache && tid >= 128 && tid < 128 + RG_BANDLO16)
-            cpf = *(const uint4 *)(scache + (size_t)(y0 / 4) * RG_LOROW + 16 * (tid - 128));
+        if (use_cache && tid >= RG_CPF0 && tid < RG_CPF0 + RG_BANDLO16)
+            cpf = *(const uint4 *)(scache + (size_t)(y0 / 4) * RG_LOROW + 16 * (tid - RG_CPF0));
     };
     // band 0 prologue: outline layer cleared (it overlays the setup scratch: after the binning's
     // counters are done with), band list, prefetch (later bands: in the previous band's tail)
@@ -945,7 +961,8 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
 #endif
     RG_SYNC();
     const int band0 = __builtin_amdgcn_readfirstlane(sm.brng[0]), band1 = __builtin_amdgcn_readfirstlane(sm.brng[1]);
-    if (brange) {   // the static layer's rows outside [band0, band1): 36 x 16 B per band, 4 per thread per round
+    if (RG_CPF0 < 128 && tid < 128 && band0 < band1) cache_prefetch(RG_BAND * band0);   // the prefetch threads below wave 2
+    if (brange) {   // the static layer's rows outside [band0, band1): RG_BANDLO16 x 16 B per band, 4 per thread per round
         const int nst = (RG_NBANDS - (band1 - band0)) * RG_BANDLO16;
         for (int i0 = tid; i0 < nst; i0 += 4 * RG_THREADS) {
             uint4 v[4];
@@ -976,8 +993,8 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         // barrier below); a band that no body geom reaches is the static layer's rows
         const uint32_t *dmb = sm.dmask[band_i & 1];
         const bool sband = use_cache && __builtin_amdgcn_readfirstlane(dmb[0] | dmb[1] | dmb[2]) == 0u;
-        if (use_cache && tid >= 128 && tid < 128 + RG_BANDLO16)
-            sm.u.post.lo[tid - 128] = out.scache_mode == 2 ? make_uint4(0x55555555u, 0x55555555u, 0x55555555u, 0x55555555u) : cpf;
+        if (use_cache && tid >= RG_CPF0 && tid < RG_CPF0 + RG_BANDLO16)
+            sm.u.post.lo[tid - RG_CPF0] = out.scache_mode == 2 ? make_uint4(0x55555555u, 0x55555555u, 0x55555555u, 0x55555555u) : cpf;
         // (wave 1; the outline items run on waves 0 and 2 at the same time)
         const bool fwave = tid >= 64 && tid < 128;
         const int lt = tid < 64 ? tid : tid - 64;   // outline-item thread index (waves 0, 2)
@@ -1070,9 +1087,9 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         const bool need = !use_cache || ((dmb[ox >> 5] >> (ox & 31)) & 1u);
         // pass 0: the frame (skipped where the static layer stands); pass 1 (the episode's first allo frame):
         // the static layer, the body-less entities alone
-        auto resolve = [&](auto sonly_c) {
+        auto resolve = [&](auto sonly_c, int oy) {
             constexpr bool sonly = decltype(sonly_c)::value;
-            const int yb = 4 * oyl, ya = y0 + yb;
+            const int yb = 4 * oy, ya = y0 + yb, lpix = oy * MG_LORES + ox;
             uint32_t o[4][4];
 #pragma unroll
             for (int r = 0; r < 4; r++)
@@ -1121,12 +1138,13 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                 } else {
                     // the highest entity bit of each pixel -> that entity's outline ordinal (oord1[0] = 0)
                     uint32_t w0, w1;
-                    if constexpr (SM::MPW == 4) { w0 = sm.u.post.band[yb + r][ox]; w1 = 0u; }
+                    if constexpr (SM::MPW == 8) { w0 = sm.u.post.band[yb + r][ox >> 1] >> (16 * (ox & 1)); w1 = 0u; }
+                    else if constexpr (SM::MPW == 4) { w0 = sm.u.post.band[yb + r][ox]; w1 = 0u; }
                     else { const uint2 t = *(const uint2 *)&sm.u.post.band[yb + r][2 * ox]; w0 = t.x; w1 = t.y; }
                     if (w0 | w1) {
 #pragma unroll
                         for (int c = 0; c < 4; c++) {
-                            const uint32_t wc = (SM::MPW == 4 || c < 2) ? w0 : w1;
+                            const uint32_t wc = (SM::MPW >= 4 || c < 2) ? w0 : w1;
                             const uint32_t m = (wc >> (SM::MBITS * (c % SM::MPW))) & (sonly ? sm.smask : SM::MMASK);
                             const uint32_t oo = sm.oord1[m ? 32 - __clz((int)m) : 0];
                             o[r][c] = o[r][c] > oo ? o[r][c] : oo;
@@ -1161,12 +1179,20 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                     if (RG_OFS) v8 = (uint8_t)((ss + 7 + ((ss >> 4) & 1)) >> 4);
                     else { const int q = ss >> 4, rm = ss & 15; v8 = (uint8_t)(q + (rm > 8 || (rm == 8 && (q & 1)))); }
                     dst8[lpix * 3 + ch] = v8;
-                    if (WIN && pl8) pl8[ch * (2 * MG_LORES) + lpix] = v8;
+                    if (WIN && pl8) pl8[ch * (RG_BROWS * MG_LORES) + lpix] = v8;
                 }
             }
         };
-        if (need) resolve(std::false_type{});
-        if (mk_cache) resolve(std::true_type{});
+        if constexpr (RG_BROWS == 2) {
+            if (need) resolve(std::false_type{}, oyl);
+            if (mk_cache) resolve(std::true_type{}, oyl);
+        } else {   // 16-row bands: block rows oyl and oyl + 2, one after the other (registers)
+#pragma unroll 1
+            for (int oy = oyl; oy < RG_BROWS; oy += 2) {
+                if (need) resolve(std::false_type{}, oy);
+                if (mk_cache) resolve(std::true_type{}, oy);
+            }
+        }
         MG_PROF_MAXW(sm.pw[1], t_fill);
         RG_SYNC();
         MG_PROF(3);
@@ -1183,11 +1209,11 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
             ((uint4 *)&sm.u.post.band[0][0])[i] = make_uint4(0, 0, 0, 0);
         if (tid == 0) sm.nlong = 0;
         if (mode == 0 && !(dskip & 4)) {
-            if (tid >= 64) {
+            if (tid >= RG_RING0) {
                 // ring of the last 4 LoRes frames: slot nh (all 4 slots at episode start)
                 const int nring = keep_ring ? (fresh ? 4 : 1) * RG_BANDLO16 : 0;
                 const int nplain = nring + (plain ? RG_BANDLO16 : 0);
-                for (int t = tid - 64; t < nplain + (mk_cache ? RG_BANDLO16 : 0); t += RG_THREADS - 64) {
+                for (int t = tid - RG_RING0; t < nplain + (mk_cache ? RG_BANDLO16 : 0); t += RG_THREADS - RG_RING0) {
                     if (t < nring) {
                         const int sl = fresh ? t / RG_BANDLO16 : nh, c = t % RG_BANDLO16;
                         *(uint4 *)(ring + ((size_t)sl * S.N + e) * FR + lrow + 16 * c) = sm.u.post.lo[c];
@@ -1200,17 +1226,17 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
                     }
                 }
             } else if (win) {
-                // window ring: the band's 2 LoRes rows of each colour plane (2 x 96 B, planar in `los` since the
+                // window ring: the band's LoRes rows of each colour plane (RG_BROWS x 96 B, planar in `los` since the
                 // resolve) into every slot of this step's frame (fresh: of frames t-3 .. t; the slot lists come
-                // from the host, RenderOut::wsl), by wave 0 (the stack's wave): 36 x 16 B per slot
+                // from the host, RenderOut::wsl), by the stack's threads: RG_BANDLO16 x 16 B per slot
                 const int lst = fresh ? 1 : 0, nwin = out.wnsl[lst] * RG_BANDLO16;
-                for (int t = tid; t < nwin; t += 64) {
+                for (int t = tid; t < nwin; t += RG_RING0) {
                     const int slot = out.wsl[lst][t / RG_BANDLO16];
-                    const int c = t % RG_BANDLO16, pl = c / 12, j = c % 12;   // plane, 16-byte chunk of its 192 B
+                    const int c = t % RG_BANDLO16, pl = c / (RG_BANDLO16 / 3), j = c % (RG_BANDLO16 / 3);   // plane, its 16-byte chunk
                     *(uint4 *)(wring + ((size_t)e * (out.wK + 3) + slot) * FR + (size_t)pl * (MG_LORES * MG_LORES) +
                                (size_t)(y0 / 4) * MG_LORES + 16 * j) = sm.u.post.los[c];
                 }
-            } else if (stacked && tid < 2 * MG_LORES / 4 && !(dskip & 64)) {
+            } else if (stacked && tid < RG_STKT && !(dskip & 64)) {
                 // FlattenFrameStack: [96][96][12] = frames oldest..newest concatenated per pixel; one thread
                 // per 4 pixels: 3 dwords of each frame in, 12 dwords (3 x 16 B) out
                 const uint32_t *c32 = (const uint32_t *)sm.u.post.lo;
