@@ -358,6 +358,9 @@ def main():
     emulate = args.emulate_world if world == 1 and args.emulate_world > 1 else 0
     gather = (world > 1 or emulate > 0) if args.gather is None else (args.gather and (world > 1 or emulate > 0))
     chunks = int(args.chunks) if args.chunks != "auto" else pipeline.default_chunks(spec, n)
+    if gather and args.chunks == "auto":
+        # the exchange takes a stream of its own: 2 chunk streams + it + the caller's fit the 4 hardware queues
+        chunks = min(chunks, 2)
     if gather:
         from magical_amd import dist as mdist
         shard = mdist.ShardedVecEnv(args.env, n, rank=rank, device=str(device), gather=True,

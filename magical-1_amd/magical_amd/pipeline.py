@@ -33,11 +33,18 @@ PIPELINED_TASKS = ("MoveToRegion", "MoveToCorner")
 
 
 def default_chunks(spec, num_envs):
-    """bench.py --chunks auto: 2 for the robot scenes at >= 2048 envs, else 1.  (Round 6: a third MoveToRegion
-    chunk measured 3.16 -> 3.19 M env-steps/s at 4096 envs, within 1%, but its 1365-env renders fill 1.2 rounds of
-    the CUs' workgroup slots, so the dominant kernel's isolated HBM fraction reads 0.061 instead of 0.069; kept
-    at 2, profiles/r06_d, profiles/r06_final.)"""
-    return 2 if spec.task in PIPELINED_TASKS and num_envs >= 2048 and num_envs % 2 == 0 else 1
+    """bench.py --chunks auto: 3 for MoveToRegion at >= 4096 envs, 2 for the robot scenes at >= 2048, else 1.
+    (Round 6, with the 16-row-band render: a third chunk measured MoveToRegion 3.37 -> 3.42 M env-steps/s at 4096
+    envs, two repetitions (profiles/r06_b16/chunks_b16), its render-bound pipeline gaining from the smaller step
+    launches; MoveToCorner, whose pipeline is step-bound, 2.59 -> 2.61 M, within noise, and its 0.74 ms step kernel
+    then serves 1365 envs instead of 2048 -- kept at 2.  Before the 16-row render, MoveToRegion's third chunk was
+    3.16 -> 3.19 M (profiles/r06_d).  A 1365-env chunk's render fills 1.2 rounds of the CUs' workgroup slots, so its
+    isolated HBM fraction reads lower than a 2048-env chunk's.)"""
+    if spec.task not in PIPELINED_TASKS:
+        return 1
+    if spec.task == "MoveToRegion" and num_envs >= 4096:
+        return 3
+    return 2 if num_envs >= 2048 and num_envs % 2 == 0 else 1
 
 
 class PipelinedVecEnv:

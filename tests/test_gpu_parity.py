@@ -440,7 +440,8 @@ def test_window_stacks_match_materialised(name, n, L):
                                           ("MoveToCorner-Demo-LoRes4E-v0", 4096, 165)])
 def test_full_size_pipelined_parity(name, n, steps):
     """The configuration bench.py times for C2 / C3: magical_amd.pipeline.PipelinedVecEnv
-    with bench.py's own chunking (pipeline.default_chunks: 2 chunks of 2048 envs; the 8-envs-per-workgroup step
+    with bench.py's own chunking (pipeline.default_chunks: MoveToRegion 3 chunks of 1360-1376 envs, MoveToCorner 2 of
+    2048; the 8-envs-per-workgroup step
     forms 5 / 6 and the auto-reset fused into the step kernel),
     episode phases spread over the envs the oracle does not follow (so every step mixes resetting and running
     envs in a workgroup), against the oracle every step on a spread of envs of every chunk: observations

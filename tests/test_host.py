@@ -646,9 +646,10 @@ def test_latexify_results_matches_reference():
 
 
 def test_pipeline_default_chunks():
-    """bench.py --chunks auto: the robot scenes pipeline 2 chunks at >= 2048 envs, every other scene runs 1."""
+    """bench.py --chunks auto: MoveToRegion pipelines 3 chunks at >= 4096 envs, the robot scenes 2 at >= 2048
+    (2 at most under the multi-GPU exchange: bench.py), every other scene runs 1."""
     from magical_amd import pipeline
-    assert pipeline.default_chunks(registry.lookup("MoveToRegion-Demo-LoRes4E-v0"), 4096) == 2
+    assert pipeline.default_chunks(registry.lookup("MoveToRegion-Demo-LoRes4E-v0"), 4096) == 3
     assert pipeline.default_chunks(registry.lookup("MoveToRegion-Demo-LoRes4E-v0"), 2048) == 2
     assert pipeline.default_chunks(registry.lookup("MoveToCorner-Demo-LoRes4E-v0"), 4096) == 2
     assert pipeline.default_chunks(registry.lookup("MoveToRegion-Demo-LoRes4E-v0"), 64) == 1
