@@ -105,6 +105,7 @@ struct RenderSmem {
                          RG_MAXSEDGE = MAXSEDGE_, RG_MAXE = MAXE_;
     static constexpr int MBITS = MBITS_, MPW = 32 / MBITS_;   // bits / pixels per word of the outline layer
     static_assert(BAND_ == 8 || BAND_ == 16, "bands of 8 or 16 rows");
+    static_assert(MAXVERT_ <= 0x2000, "solid-edge entries hold the vertex in 13 bits");
     static constexpr int BAND = BAND_, NBANDS = MG_RES / BAND_, BROWS = BAND_ / 4;   // rows, bands, LoRes rows per band
     static constexpr int BANDLO16 = BROWS * RG_LOROW / 16;   // 16-byte chunks of a band's LoRes rows (36 / 72)
     static constexpr uint32_t MMASK = (1u << MBITS) - 1u;
@@ -126,6 +127,7 @@ struct RenderSmem {
             double dedge[RG_MAXDE][4];               // dashed outline edges (pixel-space end points) ...
             int32_t dedge_o[RG_MAXDE];               // ... and their outline-layer value
             int32_t ndedge;
+            int32_t nconv;                           // line-list slots taken by pre-clipped solid edges
         } pre;
         struct {
             uint32_t band[BAND][MG_RES / MPW]; // outline layer of the current band (entity bits per pixel)
@@ -147,7 +149,7 @@ struct RenderSmem {
     int16_t vx[RG_MAXVERT], vy[RG_MAXVERT];   // int pixel vertices (pygame (int) truncation)
     uint8_t fdelta[RG_MAXVERT];               // float->int minus double->int of x (bits 0-1) / y (2-3), +1
     uint8_t v_geom[RG_MAXVERT];
-    uint16_t sedge[RG_MAXSEDGE];              // solid outline edges: start vertex | last << 14 | inside << 15
+    uint16_t sedge[RG_MAXSEDGE];              // solid outline edges: start vertex | lines << 13 | last << 14 | inside << 15
     int16_t blist[RG_MAXG];                   // geoms overlapping the current band, in draw order
     uint32_t bxr[RG_MAXG];                    // x range of each band-list slot's geom (ginfo.y)
     int16_t dash[RG_MAXDASH][4];              // clipped dashed-outline lines
@@ -383,7 +385,7 @@ MG_DEV void segment_band(SM &sm, int x1, int y1, int x2, int y2, uint32_t ord, i
 template <class SM>
 MG_DEV void edge_ends(const SM &sm, int k, int &x1, int &y1, int &x2, int &y2, uint32_t &ord, bool &inside) {
     const uint32_t se = sm.sedge[k];
-    const int v = se & 0x3FFF, g = sm.v_geom[v];
+    const int v = se & 0x1FFF, g = sm.v_geom[v];
     const int fd = sm.fdelta[v];
     x1 = sm.vx[v] + (fd & 3) - 1; y1 = sm.vy[v] + ((fd >> 2) & 3) - 1;
     if (se & 0x4000u) { const int nx = sm.g_voff[g]; x2 = sm.vx[nx]; y2 = sm.vy[nx]; } // closing edge
@@ -396,6 +398,7 @@ MG_DEV void edge_ends(const SM &sm, int k, int &x1, int &y1, int &x2, int &y2, u
 template <class SM>
 MG_DEV void item_rows(const SM &sm, int i, int &ylo, int &yhi) {
     if (i < sm.nsedge) {
+        if (sm.sedge[i] & 0x2000u) { ylo = 1; yhi = 0; return; }   // drawn from the line list (pre-clipped)
         int x1, y1, x2, y2;
         uint32_t ord;
         bool inside;
@@ -536,7 +539,7 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         sm.u.pre.ocnt[tid] = 0;
     }
     if (tid == 0) {
-        sm.err = 0; sm.ndash = 0; sm.nsedge = 0; sm.nlong = 0; sm.u.pre.ndedge = 0;
+        sm.err = 0; sm.ndash = 0; sm.nsedge = 0; sm.nlong = 0; sm.u.pre.ndedge = 0; sm.u.pre.nconv = 0;
         sm.col[0] = pack_rgb(L->background);
         sm.u.pre.e_g0[0] = 0;
     }
@@ -719,6 +722,32 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
         }
     }
     RG_SYNC();
+    // solid outline edges that leave the surface: clip_and_draw_line_width's two sub-lines (the base line and the
+    // +1 copy across the major axis) clipped once here into the line list, where they are drawn as the dash lines
+    // are, instead of clipped again in every band they cross.  The list's free slots are taken in pairs; an edge
+    // that finds none stays a solid edge clipped per band.  Invisible sub-lines keep their slot with rows -1.
+    const int ndash0 = sm.ndash, dfree = SM::RG_MAXDASH - (ndash0 < SM::RG_MAXDASH ? ndash0 : SM::RG_MAXDASH);
+    for (int i = tid; i < sm.nsedge && i < SM::RG_MAXSEDGE; i += RG_THREADS) {
+        int x1, y1, x2, y2;
+        uint32_t ord;
+        bool inside;
+        edge_ends(sm, i, x1, y1, x2, y2, ord, inside);
+        const int ylo = y1 < y2 ? y1 : y2, yhi = (y1 > y2 ? y1 : y2) + 1;
+        const int xl = x1 < x2 ? x1 : x2, xh = x1 > x2 ? x1 : x2;
+        if (xl >= 0 && xh + 1 <= MG_RES - 1 && ylo >= 0 && yhi <= MG_RES - 1) { sm.sedge[i] |= 0x8000u; continue; }
+        const int q = atomicAdd(&sm.u.pre.nconv, 2);
+        if (q + 2 > dfree) continue;
+        const bool xmaj = abs(x1 - x2) > abs(y1 - y2);
+        for (int c = 0; c < 2; c++) {
+            int a1 = x1 + ((c && !xmaj) ? 1 : 0), b1 = y1 + ((c && xmaj) ? 1 : 0);
+            int a2 = x2 + ((c && !xmaj) ? 1 : 0), b2 = y2 + ((c && xmaj) ? 1 : 0);
+            int16_t *d = sm.dash[ndash0 + q + c];
+            if (!clipline(a1, b1, a2, b2)) { a1 = a2 = -1; b1 = b2 = -1; }
+            d[0] = (int16_t)a1; d[1] = (int16_t)b1; d[2] = (int16_t)a2; d[3] = (int16_t)b2;
+            sm.dash_o[ndash0 + q + c] = (uint16_t)ord;
+        }
+        sm.sedge[i] |= 0x2000u;
+    }
     for (int v = tid; v < NV; v += RG_THREADS) {
         const int g = sm.v_geom[v], v0 = sm.g_voff[g], n = sm.g_nv[g];
         int32_t *b = sm.u.pre.gbb[g];
@@ -746,18 +775,11 @@ render_kernel(MGState S, const mg_library *__restrict__ L, RenderOut out) {
     }
     if (sm.ndash > SM::RG_MAXDASH) sm.err = 1;
     if (sm.nsedge > SM::RG_MAXSEDGE) sm.err = 5;
-    const int nitems = sm.nsedge + (sm.ndash < SM::RG_MAXDASH ? sm.ndash : SM::RG_MAXDASH);
+    const int nlines = ndash0 + min(sm.u.pre.nconv, dfree & ~1);   // dash lines + pre-clipped solid sub-lines
+    const int nitems = sm.nsedge + (nlines < SM::RG_MAXDASH ? nlines : SM::RG_MAXDASH);
     for (int i = tid; i < nitems; i += RG_THREADS) {
         int ylo, yhi;
         item_rows(sm, i, ylo, yhi);
-        if (i < sm.nsedge) { // both width-2 sub-lines inside the surface: clipping is the identity
-            int x1, y1, x2, y2;
-            uint32_t ord;
-            bool inside;
-            edge_ends(sm, i, x1, y1, x2, y2, ord, inside);
-            int xl = x1 < x2 ? x1 : x2, xh = x1 > x2 ? x1 : x2;
-            if (xl >= 0 && xh + 1 <= MG_RES - 1 && ylo >= 0 && yhi <= MG_RES - 1) sm.sedge[i] |= 0x8000u;
-        }
         ylo = ylo > 0 ? ylo : 0; yhi = yhi < MG_RES - 1 ? yhi : MG_RES - 1;
         for (int b = ylo / RG_BAND; b <= yhi / RG_BAND && ylo <= yhi; b++) atomicAdd(&sm.u.pre.bin_cnt[b], 1);
     }
