@@ -305,14 +305,13 @@ static int pick_step_variant(const StepCaps &c, int n_envs, int task) {
     return v;
 }
 
-// The robot scenes' forms (5 / 6) take the most envs per workgroup whose grid still reaches every CU: 16 at
-// 4096 envs and more (8 measured slower there: two workgroups per CU, 0.83 vs 0.61 ms), 8 below 16 envs x CUs
-// (a workgroup then takes half a CU's LDS, so render workgroups of another env chunk fit beside it; the pipelined
-// pool's 2048-env chunks: MoveToRegion 2.82 -> 2.84 M env-steps/s, profiles/r04_check7/), 4 below 8 envs x CUs
-// (MoveToRegion's 1365-env chunks: 3.47 -> 3.54 M, profiles/r06_blk4/).
+// Robot-only scenes (variant 5) below 16 envs x CUs run 8 envs per workgroup: the grid then still reaches
+// every CU, and a workgroup takes half a CU's LDS, so render workgroups of another env chunk fit beside it
+// (the pipelined pool's 2048-env chunks: MoveToRegion 2.82 -> 2.84 M env-steps/s, profiles/r04_check7/).  At 4096 envs and more,
+// 16 (8 measured slower there: two workgroups per CU, 0.83 vs 0.61 ms).
 static int pick_step_blk(int variant, int n_envs, int cus) {
     int b = variant == 0 ? 64 : variant == 3 || variant == 4 ? 1 : 16;
-    if ((variant == 5 || variant == 6) && n_envs < 16 * cus) b = n_envs < 8 * cus ? 4 : 8;
+    if ((variant == 5 || variant == 6) && n_envs < 16 * cus) b = 8;
     const char *ov = getenv(variant == 0 ? "MG_STEP_BLK0" : "MG_STEP_BLK"); // experiments
     if (ov && mg_step_blk_ok(variant, atoi(ov))) b = atoi(ov);
     return b;

@@ -121,8 +121,7 @@ def test_rollout_parity(name, n, steps):
 KERNEL_FORMS = [
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "8"}),
     # 4 lanes per env (16 envs per 64-lane workgroup; 70 envs leave shadow lanes in the last one)
-    ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5"}),   # 4 envs per workgroup (small grid)
-    ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5", "MG_STEP_BLK": "8"}),
+    ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5"}),   # 8 envs per workgroup (small grid)
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5", "MG_STEP_BLK": "16"}),
     ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "6", "MG_STEP_BLK": "16"}),
     # robot + block scenes at 8 / 4 envs per workgroup (8 / 16 lanes per env; 8 is the default below 16 envs
