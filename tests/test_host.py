@@ -645,6 +645,32 @@ def test_latexify_results_matches_reference():
     assert str(ei.value) == ref["duplicate"]["error"]
 
 
+def test_small_render_class_holds_every_robot_scene():
+    """The small render class (RG_SMALL, mg_render.h) has no successor in the class chain: an (env, view) it cannot
+    hold is an env error.  Its caps must cover every MoveToRegion / MoveToCorner scene the library can build: robot +
+    arena + goal, or robot + arena + a block of any shape type (geoms, vertices, solid outline edges, entities,
+    outline-mask bits)."""
+    from magical_amd import tables as T
+    src = open(os.path.join(ROOT, "magical-1_amd", "csrc", "mg_render.h")).read()
+    caps = re.search(r"#define RG_SMALL ([^\n]+)", src).group(1).split(",")
+    maxg, maxvert, _maxdash, _maxbin, maxsedge, maxe = (int(x) for x in caps[:6])
+    band, mbits = int(caps[7]), int(caps[8])
+    assert band == 16 and mbits >= 3
+    L = T.build_library()
+
+    def size(r0, n):
+        polys = [L.rpoly[i] for i in range(r0, r0 + n)]
+        return (n, sum(p.npts for p in polys), sum(p.npts for p in polys if p.outline == T.OUTLINE_SOLID))
+
+    base = [size(L.robot_rpoly0, L.robot_nrpoly), size(L.arena_rpoly0, L.arena_nrpoly)]
+    scenes = [base + [size(L.goal_rpoly0, L.goal_nrpoly)]]                                       # MoveToRegion
+    scenes += [base + [size(L.block_rpoly0[t], L.block_nrpoly[t])] for t in range(T.NUM_SHAPE_TYPES)]  # MoveToCorner
+    for sc in scenes:
+        g, v, se = (sum(x[k] for x in sc) for k in range(3))
+        assert g <= maxg and v <= maxvert and se <= maxsedge and len(sc) <= min(maxe, mbits), (sc, caps)
+    assert max(sum(x[0] for x in sc) for sc in scenes) == 26 and max(sum(x[1] for x in sc) for sc in scenes) == 636
+
+
 def test_pipeline_default_chunks():
     """bench.py --chunks auto: MoveToRegion pipelines 3 chunks at >= 4096 envs, the robot scenes 2 at >= 2048
     (2 at most under the multi-GPU exchange: bench.py), every other scene runs 1."""
