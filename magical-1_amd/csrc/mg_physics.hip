@@ -47,7 +47,8 @@ bool mg_step_blk_ok(int variant, int blk) {
     return variant == 0 ? (blk == 1 || blk == 8 || blk == 64)
          : variant == 4 ? blk == 1
          : variant == 5 ? (blk == 16 || blk == 8)     // 8: grids below 16 envs per CU (mg_sim.hip pick_step_blk)
-         : variant == 6 ? (blk == 16 || blk == 8 || blk == 4)   // 4: forms test only
+         : variant == 6 ? (blk == 16 || blk == 8)     // (4 envs per workgroup, 16 lanes per env: removed in round 6,
+                                                      // profiles/r06_blk4)
          : false;
 }
 
@@ -58,7 +59,7 @@ hipError_t mg_launch_step(const MGState &S, const mg_library *L, TaskCfg cfg, in
     if (variant == V && blk == B) \
         return launch_step_var<V, B>(S, L, cfg, max_steps, auto_reset, actions, reward, done, eval_score, reset_mask, st);
     MG_STEP_CASE(4, 1)
-    MG_STEP_CASE(5, 16) MG_STEP_CASE(5, 8) MG_STEP_CASE(6, 16) MG_STEP_CASE(6, 8) MG_STEP_CASE(6, 4)
+    MG_STEP_CASE(5, 16) MG_STEP_CASE(5, 8) MG_STEP_CASE(6, 16) MG_STEP_CASE(6, 8)
     MG_STEP_CASE(0, 1) MG_STEP_CASE(0, 8) MG_STEP_CASE(0, 64)
 #undef MG_STEP_CASE
     return hipErrorInvalidValue;

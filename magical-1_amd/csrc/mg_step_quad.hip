@@ -7,6 +7,4 @@ template hipError_t launch_step_var<6, 16>(const MGState &, const mg_library *, 
 // 8 envs per workgroup (half the LDS): robot-scene grids below 16 envs per CU (mg_sim.hip pick_step_blk)
 template hipError_t launch_step_var<5, 8>(const MGState &, const mg_library *, TaskCfg, int, int, const uint8_t *, float *, uint8_t *, double *, uint8_t *, hipStream_t);
 template hipError_t launch_step_var<6, 8>(const MGState &, const mg_library *, TaskCfg, int, int, const uint8_t *, float *, uint8_t *, double *, uint8_t *, hipStream_t);
-// 4 envs per workgroup (16 lanes per env): forms test only
-template hipError_t launch_step_var<6, 4>(const MGState &, const mg_library *, TaskCfg, int, int, const uint8_t *, float *, uint8_t *, double *, uint8_t *, hipStream_t);
 MG_PROF_READER(mg_prof_read_step_quad)

@@ -124,10 +124,11 @@ KERNEL_FORMS = [
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5"}),   # 8 envs per workgroup (small grid)
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "5", "MG_STEP_BLK": "16"}),
     ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "6", "MG_STEP_BLK": "16"}),
-    # robot + block scenes at 8 / 4 envs per workgroup (8 / 16 lanes per env; 8 is the default below 16 envs
-    # per CU, the pipelined pool's 2048-env chunks): removed in round 4 after a GPU fault, restored in round 5
+    # robot + block scenes at 8 envs per workgroup (8 lanes per env; the default below 16 envs per CU, the
+    # pipelined pool's 2048-env chunks): removed in round 4 after a GPU fault, restored in round 5.  The 4-env
+    # workgroups (16 lanes per env) were removed in round 6 after an unexplained fault of form 5/4
+    # (profiles/r06_blk4)
     ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "6", "MG_STEP_BLK": "8"}),
-    ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "6", "MG_STEP_BLK": "4"}),
     ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, {"MG_STEP_VARIANT": "0", "MG_STEP_BLK0": "1"}),
     ("ClusterColour-Demo-LoResStack-v0", 66, 30, {"MG_STEP_VARIANT": "4"}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 30, {"MG_STEP_VARIANT": "4"}),
