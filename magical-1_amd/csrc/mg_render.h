@@ -28,8 +28,10 @@
 // 26 geoms (star block), 636 vertices (circle block), 204 solid outline edges, 3 entities) in 16-row bands with
 // a 4-bit outline mask: 17.4 KB, 9 workgroups/CU (round 6: the 8-row class took 16.2 KB at 9 per CU; 16-row bands
 // halve the bands' barriers, band lists and per-band edge / segment set-up, render 0.628 -> 0.553 ms per 2048-env
-// chunk, MoveToRegion 3.16 -> 3.37 M env-steps/s, profiles/r06_b16).  The many-block classes stay at 8 rows:
-// 16-row medium-0 / medium-1 (6 / 5 per CU) measured 15% / 6% slower (ClusterColour / MatchRegions).
+// chunk, MoveToRegion 3.16 -> 3.37 M env-steps/s, profiles/r06_b16).  Medium-0 / medium-1 stay at 8 rows: at 16 (6 / 5
+// per CU) they measured 15% / 6% slower (ClusterColour / MatchRegions), their launches being throughput-bound.  The
+// medium-2 launch renders only the pairs the earlier classes hand over (MatchRegions-TestAll: ~8%) and is bound by
+// its slowest workgroups, so the shorter 16-row workgroups pay there: MatchRegions 1.449 -> 1.462 M (profiles/r06_m2b16).
 #define RG_LARGE 160, 1600, 256, 3072, 1600, MG_MAX_ENTS, uint32_t
 #ifndef RG_MEDIUM0
 #define RG_MEDIUM0 44, 784, 128, 1280, 512, MG_MAX_ENTS, uint16_t   // 20.3 KB: 8 workgroups/CU
@@ -37,7 +39,9 @@
 #ifndef RG_MEDIUM1
 #define RG_MEDIUM1 48, 896, 160, 1536, 512, MG_MAX_ENTS, uint16_t
 #endif
-#define RG_MEDIUM2 96, 1280, 160, 2560, 768, MG_MAX_ENTS, uint16_t
+#ifndef RG_MEDIUM2
+#define RG_MEDIUM2 96, 1280, 160, 2560, 768, MG_MAX_ENTS, uint16_t, 16   // 16-row bands: see below
+#endif
 #ifndef RG_SMALL
 #define RG_SMALL 28, 640, 160, 1536, 208, 4, uint8_t, 16, 4
 #endif
