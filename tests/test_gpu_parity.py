@@ -924,6 +924,108 @@ def test_packed_gather_pipeline_single_rank(tmp_path, name, mode, L, opts):
         dist.destroy_process_group()
 
 
+TWO_RANK_WORKER = r"""
+import os, sys
+sys.path[:0] = [{root!r} + "/magical-1_amd"]
+import numpy as np, torch, torch.distributed as dist
+import magical_amd
+from magical_amd import dist as mdist
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", init_method="env://")
+name, mode, L, opts, n, steps = {name!r}, {mode!r}, {L}, {opts!r}, {n}, {steps}
+shard = mdist.ShardedVecEnv(name, n, rank=rank, device="cuda:0", gather=True, gather_mode=mode,
+                            max_episode_steps=L, **opts)
+window = isinstance(getattr(shard, "restacker", None), mdist.WindowRestacker)
+lag = 0 if window else 1
+acts = np.random.RandomState(4).randint(0, 18, (steps, world * n))
+lo, hi = mdist.shard_range(n, rank)
+# rank 0 checks every gathered step against one process running all world * n envs (env i seeded 1000 + i)
+ref = magical_amd.make_vec(name, world * n, seeds=list(range(1000, 1000 + world * n)), max_episode_steps=L) \
+    if rank == 0 else None
+bad = []
+def check(tag, got, want):
+    for k in want[0]:
+        g = got[0][k].reshape((world * n,) + tuple(want[0][k].shape[1:]))
+        if not torch.equal(g, want[0][k]):
+            bad.append(f"{{tag}} {{k}}")
+    if len(want) > 1:
+        for i, key in ((1, "reward"), (2, "done")):
+            if not torch.equal(got[i].reshape(-1), want[i]):
+                bad.append(f"{{tag}} {{key}}")
+        if not torch.equal(got[3]["eval_score"].reshape(-1), want[3]["eval_score"]):
+            bad.append(f"{{tag}} eval_score")
+got = shard.reset()
+if rank == 0:
+    check("reset", (got,), (ref.reset(),))
+handles, prev, resets = [], {{}}, 0
+for t in range(steps):
+    handles.append(shard.step_async(torch.as_tensor(acts[t, lo:hi], dtype=torch.uint8)))
+    if rank == 0:
+        obs, rew, done, info = ref.step(torch.as_tensor(acts[t], dtype=torch.uint8))
+        resets += int(done.sum().item())
+        prev[t] = ({{k: v.clone() for k, v in obs.items()}}, rew.clone(), done.clone(),
+                   {{"eval_score": info["eval_score"].clone()}})
+    u = t - lag
+    if u >= 0:
+        r = handles[u].results()
+        if rank == 0:
+            check(f"step {{u}}", r, prev.pop(u))
+if lag:
+    r = handles[-1].results()
+    if rank == 0:
+        check(f"step {{steps - 1}}", r, prev.pop(steps - 1))
+shard.close()
+dist.barrier()
+dist.destroy_process_group()
+if rank == 0:
+    print("resets", resets, "mismatches", len(bad), bad[:8], flush=True)
+    sys.exit(1 if bad or resets < world * n else 0)
+"""
+
+TWO_RANK_CASES = [("MoveToRegion-Demo-LoRes4E-v0", "frames", 12, {"chunks": 2}),   # bench.py's N > 1 path
+                  ("MoveToRegion-Demo-LoRes4E-v0", "stacked", 12, {}),
+                  ("ClusterColour-Demo-LoResStack-v0", "frames", 10, {}),
+                  ("MoveToCorner-Demo-LoRes4A-v0", "frames", 12, {"chunks": 2})]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,mode,L,opts", TWO_RANK_CASES,
+                         ids=[f"{c[0].split('-')[0]}-{c[1]}-" + "-".join(f"{k}{v}" for k, v in c[3].items())
+                              for c in TWO_RANK_CASES])
+def test_two_rank_gather_on_one_gpu(tmp_path, name, mode, L, opts):
+    """The multi-GPU exchange with world_size 2 (W > 1 of the GPU pool / window-ring path was unpinned):
+    two processes, each a shard of 16 envs on the simulator, exchange every step's packed outputs with
+    all_gather_into_tensor and rebuild the stacks on the receiver (window rings / materialised), the pipelined
+    pool under the gather for MoveToRegion as bench.py runs it at N > 1.  RCCL refuses two ranks on one device, so
+    the group here is gloo on the same card (the collective copies through the host); on a node each rank has its
+    own GPU and the group is RCCL.  Rank 0 checks every gathered [2, 16, ...] step -- observations incl. the rebuilt
+    stacks, reward, done, eval_score -- against one process running all 32 envs, bit for bit, across auto-resets."""
+    import socket
+    import subprocess
+    import sys
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "worker.py"
+    script.write_text(TWO_RANK_WORKER.format(root=root, name=name, mode=mode, L=L, opts=opts, n=16, steps=30))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", str(script)], env=env))
+    rcs = []
+    try:
+        for p in procs:
+            rcs.append(p.wait(timeout=150))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0, 0]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("preproc", ["LoRes4E", "LoResStack", "LoRes4A"])
 def test_restack_window_matches_oracle_rule(preproc):
