@@ -349,10 +349,16 @@ def main():
     from magical_amd import native, pipeline, registry
 
     spec = registry.lookup(args.env)
-    device = torch.device("cuda", local_rank)
+    # rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0 over a gloo group (RCCL refuses two ranks
+    # on one device); the variable is recorded in config.env_overrides, and such a line is not a node measurement
+    same_gpu = world > 1 and os.environ.get("MAGICAL_AMD_BENCH_SAME_GPU") == "1"
+    device = torch.device("cuda", 0 if same_gpu else local_rank)
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if same_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
     n = args.envs
     seeds = [1000 + rank * n + i for i in range(n)]
     emulate = args.emulate_world if world == 1 and args.emulate_world > 1 else 0
