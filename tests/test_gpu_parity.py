@@ -502,6 +502,8 @@ def test_full_size_pipelined_parity(name, n, steps):
 RESET_PATHS = [
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 40, 7, {}),
     ("MatchRegions-TestAll-LoRes4E-v0", 66, 40, 7, {"MG_RESET_PREFETCH": "0"}),
+    # the shadow -> main copy with several envs per workgroup (the default cap, 2048 workgroups, is above n here)
+    ("MatchRegions-TestAll-LoRes4E-v0", 66, 40, 7, {"MG_COPY_WG": "5"}),
     ("ClusterColour-TestAll-LoResStack-v0", 66, 30, 4, {}),
     ("MoveToRegion-Demo-LoRes4E-v0", 70, 45, 5, {"MG_RESET_PREFETCH": "1"}),
     # the robot scenes' auto-reset: fused into the step kernel (default) and as its own launch
@@ -509,6 +511,7 @@ RESET_PATHS = [
     ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, 6, {}),
     ("MoveToCorner-Demo-LoRes4E-v0", 70, 45, 6, {"MG_FUSED_RESET": "0"}),
     ("PickAndPlace-Demo-LoResCHW4A-v0", 8, 30, 4, {}),
+    ("PickAndPlace-Demo-LoResCHW4A-v0", 8, 30, 4, {"MG_COPY_WG": "3"}),
     ("FindDupe-TestAll-LoRes4E-v0", 66, 30, 1, {}),
 ]
 
